@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident RS(10,4) encode+decode on MI355X (BASELINE.json metric).
+
+Workload (N=1 line; BASELINE.json metric "GiB/s device-resident RS encode+decode
+(k=10,m=4, 1 MiB shards)"): every GPU holds `--stripes` stripes of RS(k, m) with S-byte
+shards in HBM ([stripe][shard][pitch] layout). One *step* is one pass of the hot path
+over that batch:
+  1. encode  — parity of every stripe from its k data shards     (codec.go:36)
+  2. decode  — reconstruct the erased shards (--erase, default {0,1,2,3}, the
+               worst case of configs[2]) from the first k present ones and
+               re-verify any remaining present parity               (codec.go:55,59)
+value = user bytes through both ops (2 * stripes * k * S per GPU per step) summed over
+all ranks / the max-over-ranks wall time of the timed steps, in GiB/s.
+
+Multi-GPU: one process per GPU (torch.distributed.run); stripes are independent, so
+each rank encodes/decodes its own batch with no data-path collective ("weak"
+scaling). The only cross-rank traffic is the gloo barrier and the max-reduce of the
+timer.
+
+roofline: the encode kernel's algorithmic bytes per launch ((k+m)*S per stripe) over
+its average HIP-event duration on the launch stream, against 8.0 TB/s HBM3E.
+cpu_baseline: rank 0 at N=1 only — the C port of the reference CPU algorithm
+(oracle/rs_oracle.c: upstream GFNI/AVX2 strategy, byte-range threads) on a bounded
+sample of the same stripes; the same leg checks the GPU parity of those stripes
+bit-exactly against it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "GiB/s device-resident RS encode+decode (k=10,m=4, 1 MiB shards); % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--m", type=int, default=4)
+    p.add_argument("--shard-bytes", type=int, default=1 << 20)
+    p.add_argument("--stripes", type=int, default=256, help="stripes per GPU")
+    p.add_argument("--erase", default="0,1,2,3", help="erased shard indices for decode")
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="CPU baseline time budget (0 disables)")
+    p.add_argument("--cpu-stripes", type=int, default=16)
+    p.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
+                   help="PMC-measured HBM bytes per launch (rocprofv3 --pmc), if present")
+    return p.parse_args(argv)
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def cpu_baseline(sb, k, m, erase, seconds, nstripes):
+    """Reference CPU path (port) on a bounded sample + bit-exact check of those stripes."""
+    import numpy as np
+    from oracle import cref
+    from oracle import rs_oracle as o
+
+    S = sb.S
+    ns = min(nstripes, sb.batch)
+    host = sb.buf[:ns, :, :S].cpu().numpy()  # GPU-encoded+decoded stripes
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    E = cref.encode_matrix(k, m)
+    P = E[k:]
+    present = [i not in erase for i in range(k + m)]
+    valid, missing, rows = o.decode_rows(k, m, present)
+    rows = np.array(rows, dtype=np.uint8).reshape(len(missing), k)
+
+    # correctness: CPU parity of the sampled stripes == GPU parity (bit-exact)
+    for b in range(ns):
+        par = cref.apply(P, [host[b, i] for i in range(k)], simd=True, nthreads=threads)
+        for j in range(m):
+            if not np.array_equal(par[j], host[b, k + j]):
+                raise SystemExit(f"parity mismatch vs CPU oracle: stripe {b} shard {k + j}")
+
+    # timing: upstream Encode, then Decode = Reconstruct (missing rows from the first k
+    # present) + Verify (all parity re-encoded and compared), repeated until `seconds`
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        for b in range(ns):
+            data = [host[b, i] for i in range(k)]
+            cref.apply(P, data, simd=True, nthreads=threads)
+            if len(missing):
+                cref.apply(rows, [host[b, i] for i in valid], simd=True, nthreads=threads)
+            par = cref.apply(P, data, simd=True, nthreads=threads)
+            for j in range(m):
+                if not np.array_equal(par[j], host[b, k + j]):
+                    raise SystemExit("verify mismatch")
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    user = 2 * passes * ns * k * S
+    return {
+        "value": round(user / el / 2**30, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "impl": f"oracle/rs_oracle.c orc_apply_simd ({cref.simd_kind()}, byte-range threads)",
+        "sample": (f"{ns} stripes x RS({k},{m}) x {S} B shards, encode + decode(erase "
+                   f"{sorted(erase)}: reconstruct + verify), {passes} passes in {el:.1f} s"),
+        "parity_check": f"GPU parity == CPU port, bit-exact, on {ns} sampled stripes",
+    }
+
+
+def load_traffic(path, cfg):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("config") != cfg:
+        return None, None
+    return t.get("encode_bytes_per_launch"), os.path.relpath(path, HERE)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    rank, world, local = dist_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from callfs_amd.device import Plan, StripeBatch
+
+    k, m, S, B = args.k, args.m, args.shard_bytes, args.stripes
+    erase = sorted({int(x) for x in args.erase.split(",") if x != ""})
+    present = [i not in erase for i in range(k + m)]
+
+    sb = StripeBatch(k, m, S, B, dev)
+    sb.fill_random(0xCA11F5 + rank)
+    enc = Plan.for_batch(sb)
+    dec = Plan.for_batch(sb, present=present)
+    stream = torch.cuda.current_stream(dev)
+
+    # untimed device-side round-trip check: encode, erase, decode, compare
+    enc.launch(stream)
+    ref = sb.buf[:, :, :S].clone()
+    for i in erase:
+        sb.buf[:, i, :S].zero_()
+    dec.launch(stream)
+    if dec.corrupt(stream) or not torch.equal(sb.buf[:, :, :S], ref):
+        raise SystemExit("device round trip failed")
+    del ref
+
+    for _ in range(args.warmup):
+        enc.launch(stream)
+        dec.launch(stream)
+
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev[s][0].record(stream)
+        enc.launch(stream)
+        ev[s][1].record(stream)
+        dec.launch(stream)
+        ev[s][2].record(stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    barrier()
+    torch.cuda.synchronize(dev)
+    if dec.corrupt(stream):
+        raise SystemExit("verify flagged corruption during the timed run")
+
+    el = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(el[0])
+
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    user_step = 2 * B * k * S
+    value = world * args.steps * user_step / elapsed / 2**30
+
+    cfg = {"k": k, "m": m, "shard_bytes": S, "stripes": B}
+    traffic, tsrc = load_traffic(args.traffic, cfg)
+    achieved = enc.bytes / (enc_ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: seeded uniform random bytes generated on device",
+        "config": {
+            "workload": (f"RS({k},{m}) device-resident encode + decode(erase {erase}), "
+                         f"{S} B shards, {B} stripes per GPU"),
+            **cfg,
+            "erase": erase,
+            "parallelism": f"stripes sharded over {world} GPU(s), no collective",
+        },
+        "encode_gib_s": round(world * B * k * S / (enc_ms * 1e-3) / 2**30, 2),
+        "decode_gib_s": round(world * B * k * S / (dec_ms * 1e-3) / 2**30, 2),
+        "encode_ms": round(enc_ms, 4),
+        "decode_ms": round(dec_ms, 4),
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "rs_apply_vec (encode plan)",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": tsrc,
+            "algorithmic_bytes_per_launch": enc.bytes,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        line["cpu_baseline"] = cpu_baseline(sb, k, m, erase, args.cpu_seconds, args.cpu_stripes)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    enc.close()
+    dec.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,688 @@
+// C ABI of the MI355X Reed-Solomon path (include/callfs_rs.h).
+//
+// Host side of the drop-in for erasure/codec.go. The control flow and error precedence
+// follow codec.go:21-78 and the upstream reedsolomon methods it calls (Split/Encode at
+// :31/:36, Reconstruct at :55, Verify at :59); every byte of GF(2^8) arithmetic over
+// shard data runs in the HIP kernels of rs_kernels.hip.
+//
+// Structure
+//  * rs_ctx     — selected devices, each with a pool of Lanes and a cache of decode
+//                 tables keyed by (k, m, presence mask).
+//  * Lane       — one HIP stream plus grow-only device/pinned buffers: the pitched
+//                 shard workspace used by the host-memory entry points, pointer
+//                 tables and coefficient tables for one-shot launches.
+//  * rs_plan    — device-resident tables for repeated, graph-capturable launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <list>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/callfs_rs.h"
+#include "gf256.hpp"
+#include "rs_kernels.hpp"
+
+using namespace callfs;
+
+namespace {
+
+#define HIPCHK(x)                           \
+  do {                                      \
+    if ((x) != hipSuccess) return RS_E_HIP; \
+  } while (0)
+
+constexpr size_t kPitchAlign = 256;
+constexpr int kMaxLanesPerDevice = 8;
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int check_profile(int k, int m) {
+  if (k < 1 || m < 1) return RS_E_INVALID_PROFILE;
+  if (k + m > 256) return RS_E_UNSUPPORTED;
+  return RS_OK;
+}
+
+// ---- coefficient tables -----------------------------------------------------------
+
+// One launch group: up to kMaxRowsPerLaunch output rows over the same k inputs.
+struct Group {
+  std::vector<int> shard;     // shard index per row
+  uint32_t verify_mask = 0;   // bit r: compare row r (Verify) instead of storing it
+  std::vector<uint32_t> tabs; // [k][R][5]
+};
+
+struct Tables {
+  int k = 0, m = 0;
+  std::vector<int> valid;
+  std::vector<int> missing;
+  std::vector<int> check;
+  std::vector<Group> groups;
+};
+
+// verify=false drops the check rows (plain Reconstruct).
+std::shared_ptr<const Tables> build_tables(int k, int m, const uint8_t* present, bool verify) {
+  DecodePlan dp;
+  if (!decode_plan(k, m, present, dp)) return nullptr;
+  auto t = std::make_shared<Tables>();
+  t->k = k;
+  t->m = m;
+  t->valid = dp.valid;
+  t->missing = dp.missing;
+  if (verify) t->check = dp.check;
+  const int nrows = static_cast<int>(t->missing.size() + t->check.size());
+  for (int g0 = 0; g0 < nrows; g0 += kMaxRowsPerLaunch) {
+    Group g;
+    const int R = std::min(kMaxRowsPerLaunch, nrows - g0);
+    g.tabs.assign(static_cast<size_t>(k) * R * kTabWords, 0);
+    for (int r = 0; r < R; ++r) {
+      const int row = g0 + r;
+      const bool is_check = row >= static_cast<int>(t->missing.size());
+      g.shard.push_back(is_check ? t->check[row - t->missing.size()] : t->missing[row]);
+      if (is_check) g.verify_mask |= 1u << r;
+      for (int i = 0; i < k; ++i)
+        perm_tables(dp.rows.at(row, i), &g.tabs[(static_cast<size_t>(i) * R + r) * kTabWords]);
+    }
+    t->groups.push_back(std::move(g));
+  }
+  return t;
+}
+
+class TableCache {
+ public:
+  std::shared_ptr<const Tables> get(int k, int m, const uint8_t* present, bool verify) {
+    std::string key;
+    key.reserve(k + m + 8);
+    key.append(reinterpret_cast<const char*>(&k), sizeof k);
+    key.append(reinterpret_cast<const char*>(&m), sizeof m);
+    key.push_back(verify ? 'v' : 'r');
+    for (int i = 0; i < k + m; ++i) key.push_back(present[i] ? '1' : '0');
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = map_.find(key);
+      if (it != map_.end()) return it->second;
+    }
+    auto t = build_tables(k, m, present, verify);
+    if (!t) return nullptr;
+    std::lock_guard<std::mutex> g(mu_);
+    if (map_.size() >= kCap) map_.clear();
+    map_.emplace(key, t);
+    return t;
+  }
+
+ private:
+  static constexpr size_t kCap = 4096;
+  std::mutex mu_;
+  std::unordered_map<std::string, std::shared_ptr<const Tables>> map_;
+};
+
+// ---- device buffers ------------------------------------------------------------------
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return RS_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, n) != hipSuccess) return RS_E_NOMEM;
+    cap = n;
+    return RS_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return RS_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return RS_E_NOMEM;
+    cap = n;
+    return RS_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Lane {
+  hipStream_t stream = nullptr;
+  DevBuf shards;    // pitched shard workspace (host-memory entry points)
+  HostBuf stage;    // pinned mirror of `shards`
+  DevBuf meta;      // pointer tables + coefficient tables + status word
+  HostBuf hmeta;    // pinned staging for `meta`
+};
+
+struct Device {
+  int id = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::unique_ptr<Lane>> lanes;
+  std::vector<Lane*> free_lanes;
+};
+
+// Device-side layout of everything one set of launches needs, packed into one buffer.
+struct MetaLayout {
+  size_t in_off = 0, status_off = 0, total = 0;
+  std::vector<size_t> out_off, tab_off;
+};
+
+MetaLayout meta_layout(const Tables& t, int batch) {
+  MetaLayout L;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off = round_up(off + bytes, 256);
+    return o;
+  };
+  L.status_off = take(sizeof(int));
+  L.in_off = take(sizeof(void*) * static_cast<size_t>(batch) * t.k);
+  for (const Group& g : t.groups) {
+    L.out_off.push_back(take(sizeof(void*) * static_cast<size_t>(batch) * g.shard.size()));
+    L.tab_off.push_back(take(sizeof(uint32_t) * g.tabs.size()));
+  }
+  L.total = off;
+  return L;
+}
+
+// Fill host staging for the meta buffer. shard_ptr(b, i) gives stripe b's shard i.
+template <class F>
+bool fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
+  std::memset(h + L.status_off, 0, sizeof(int));
+  auto* in = reinterpret_cast<const uint8_t**>(h + L.in_off);
+  bool aligned = true;
+  auto note = [&](const void* p) { aligned &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+  for (int b = 0; b < batch; ++b)
+    for (int i = 0; i < t.k; ++i) {
+      in[static_cast<size_t>(b) * t.k + i] = shard_ptr(b, t.valid[i]);
+      note(in[static_cast<size_t>(b) * t.k + i]);
+    }
+  for (size_t gi = 0; gi < t.groups.size(); ++gi) {
+    const Group& g = t.groups[gi];
+    auto* out = reinterpret_cast<uint8_t**>(h + L.out_off[gi]);
+    const size_t R = g.shard.size();
+    for (int b = 0; b < batch; ++b)
+      for (size_t r = 0; r < R; ++r) {
+        out[b * R + r] = const_cast<uint8_t*>(shard_ptr(b, g.shard[r]));
+        note(out[b * R + r]);
+      }
+    std::memcpy(h + L.tab_off[gi], g.tabs.data(), g.tabs.size() * sizeof(uint32_t));
+  }
+  return aligned;
+}
+
+hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_t* d, size_t S,
+                         bool aligned, hipStream_t s) {
+  for (size_t gi = 0; gi < t.groups.size(); ++gi) {
+    const Group& g = t.groups[gi];
+    ApplyArgs a{};
+    a.in_tab = reinterpret_cast<const uint8_t* const*>(d + L.in_off);
+    a.out_tab = reinterpret_cast<uint8_t* const*>(d + L.out_off[gi]);
+    a.tabs = reinterpret_cast<const uint32_t*>(d + L.tab_off[gi]);
+    a.S = S;
+    a.verify_mask = g.verify_mask;
+    a.status = reinterpret_cast<int*>(d + L.status_off);
+    a.K = t.k;
+    a.R = static_cast<int>(g.shard.size());
+    a.batch = batch;
+    hipError_t e = launch_apply(a, aligned, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+uint64_t algo_bytes(const Tables& t, size_t S, int batch) {
+  // reads: k valid shards + compared parity; writes: missing shards.
+  return static_cast<uint64_t>(batch) * S * (t.k + t.check.size() + t.missing.size());
+}
+
+}  // namespace
+
+// ---- context ------------------------------------------------------------------------
+
+struct rs_ctx {
+  std::vector<std::unique_ptr<Device>> devs;
+  std::atomic<unsigned> rr{0};
+  TableCache cache;
+
+  ~rs_ctx() {
+    for (auto& d : devs) {
+      (void)hipSetDevice(d->id);
+      for (auto& l : d->lanes) {
+        if (l->stream) (void)hipStreamSynchronize(l->stream);
+        l->shards.release();
+        l->stage.release();
+        l->meta.release();
+        l->hmeta.release();
+        if (l->stream) (void)hipStreamDestroy(l->stream);
+      }
+    }
+  }
+
+  Device* device(int id) {
+    for (auto& d : devs)
+      if (d->id == id) return d.get();
+    return nullptr;
+  }
+
+  Lane* acquire(Device* d) {
+    std::unique_lock<std::mutex> g(d->mu);
+    for (;;) {
+      if (!d->free_lanes.empty()) {
+        Lane* l = d->free_lanes.back();
+        d->free_lanes.pop_back();
+        return l;
+      }
+      if (static_cast<int>(d->lanes.size()) < kMaxLanesPerDevice) {
+        auto l = std::make_unique<Lane>();
+        if (hipSetDevice(d->id) != hipSuccess ||
+            hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess)
+          return nullptr;
+        d->lanes.push_back(std::move(l));
+        return d->lanes.back().get();
+      }
+      d->cv.wait(g);
+    }
+  }
+
+  void release(Device* d, Lane* l) {
+    {
+      std::lock_guard<std::mutex> g(d->mu);
+      d->free_lanes.push_back(l);
+    }
+    d->cv.notify_one();
+  }
+};
+
+namespace {
+
+struct LaneGuard {
+  rs_ctx* ctx;
+  Device* dev;
+  Lane* lane;
+  ~LaneGuard() {
+    if (lane) ctx->release(dev, lane);
+  }
+};
+
+// Host-memory path: stage the k valid shards into the lane's pitched workspace, run
+// every group, copy the written shards back. in(i)/out(i) give host buffers by shard
+// index. Returns RS_OK / RS_E_CORRUPT (verify rows mismatched) / error.
+template <class InF, class OutF>
+int run_host(rs_ctx* ctx, const Tables& t, size_t S, InF host_in, OutF host_out) {
+  if (ctx->devs.empty()) return RS_E_HIP;
+  Device* dev = ctx->devs[ctx->rr.fetch_add(1) % ctx->devs.size()].get();
+  LaneGuard lg{ctx, dev, ctx->acquire(dev)};
+  if (!lg.lane) return RS_E_HIP;
+  Lane& L = *lg.lane;
+  HIPCHK(hipSetDevice(dev->id));
+  const int n = t.k + t.m;
+  const size_t pitch = round_up(std::max<size_t>(S, 1), kPitchAlign);
+  int rc = L.shards.ensure(pitch * n);
+  if (rc) return rc;
+  if ((rc = L.stage.ensure(pitch * n))) return rc;
+  auto* dsh = static_cast<uint8_t*>(L.shards.p);
+  auto* hsh = static_cast<uint8_t*>(L.stage.p);
+
+  const MetaLayout ML = meta_layout(t, 1);
+  if ((rc = L.meta.ensure(ML.total))) return rc;
+  if ((rc = L.hmeta.ensure(ML.total))) return rc;
+  auto* dmeta = static_cast<uint8_t*>(L.meta.p);
+  const bool aligned = fill_meta(t, ML, 1, static_cast<uint8_t*>(L.hmeta.p),
+                                 [&](int, int i) { return dsh + pitch * i; });
+  HIPCHK(hipMemcpyAsync(dmeta, L.hmeta.p, ML.total, hipMemcpyHostToDevice, L.stream));
+
+  // inputs: valid shards + verify shards
+  std::vector<int> ins(t.valid);
+  ins.insert(ins.end(), t.check.begin(), t.check.end());
+  for (int i : ins) {
+    std::memcpy(hsh + pitch * i, host_in(i), S);
+    HIPCHK(hipMemcpyAsync(dsh + pitch * i, hsh + pitch * i, S, hipMemcpyHostToDevice, L.stream));
+  }
+  HIPCHK(launch_groups(t, ML, 1, dmeta, S, aligned, L.stream));
+  for (int i : t.missing)
+    HIPCHK(hipMemcpyAsync(hsh + pitch * i, dsh + pitch * i, S, hipMemcpyDeviceToHost, L.stream));
+  int status = 0;
+  if (!t.check.empty())
+    HIPCHK(hipMemcpyAsync(&status, dmeta + ML.status_off, sizeof(int), hipMemcpyDeviceToHost,
+                          L.stream));
+  HIPCHK(hipStreamSynchronize(L.stream));
+  for (int i : t.missing) std::memcpy(host_out(i), hsh + pitch * i, S);
+  return status ? RS_E_CORRUPT : RS_OK;
+}
+
+// Reconstruct's argument checks (upstream checkShards(shards, true)).
+int check_lens(int n, const size_t* lens, bool nilok, size_t* S, int* npresent) {
+  size_t size = 0;
+  for (int i = 0; i < n; ++i)
+    if (lens[i]) {
+      size = lens[i];
+      break;
+    }
+  if (size == 0) return RS_E_NO_DATA;
+  int np = 0;
+  for (int i = 0; i < n; ++i) {
+    if (lens[i] != size && (lens[i] != 0 || !nilok)) return RS_E_SHARD_SIZE;
+    np += lens[i] != 0;
+  }
+  *S = size;
+  *npresent = np;
+  return RS_OK;
+}
+
+// Shared by rs_reconstruct / rs_codec_decode. verify=true fuses upstream Verify.
+int reconstruct_host(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens,
+                     bool verify) {
+  const int n = k + m;
+  size_t S = 0;
+  int np = 0;
+  int rc = check_lens(n, lens, true, &S, &np);
+  if (rc) return rc;
+  if (np < k) return RS_E_TOO_FEW_SHARDS;
+  if (np == n && !verify) return RS_OK;
+  for (int i = 0; i < n; ++i)
+    if (!shards[i]) return RS_E_ARG;
+  uint8_t present[256];
+  for (int i = 0; i < n; ++i) present[i] = lens[i] != 0;
+  auto t = ctx->cache.get(k, m, present, verify);
+  if (!t) return RS_E_SINGULAR;
+  if (t->groups.empty()) return RS_OK;
+  rc = run_host(ctx, *t, S, [&](int i) { return shards[i]; }, [&](int i) { return shards[i]; });
+  if (rc == RS_OK || rc == RS_E_CORRUPT)
+    for (int i : t->missing) lens[i] = S;
+  return rc;
+}
+
+}  // namespace
+
+// ---- exported -------------------------------------------------------------------------
+
+extern "C" {
+
+int rs_abi_version(void) { return RS_ABI_VERSION; }
+
+const char* rs_strerror(int code) {
+  switch (code) {
+    case RS_OK: return "ok";
+    case RS_E_INVALID_PROFILE: return "erasure: invalid erasure profile parameters (code 3054)";
+    case RS_E_SHORT_DATA: return "not enough data to fill the number of requested shards";
+    case RS_E_TOO_FEW_SHARDS: return "too few shards given";
+    case RS_E_SHARD_SIZE: return "shard sizes do not match";
+    case RS_E_NO_DATA: return "no shard data";
+    case RS_E_CORRUPT: return "erasure: shard checksum mismatch (code 3051)";
+    case RS_E_INSUFFICIENT: return "erasure: insufficient shards for reconstruction (code 3050)";
+    case RS_E_UNSUPPORTED: return "profile needs the GF(2^16) (Leopard) codec: k+m > 256";
+    case RS_E_HIP: return "HIP runtime error or no usable device";
+    case RS_E_ARG: return "invalid argument";
+    case RS_E_SINGULAR: return "matrix is singular";
+    case RS_E_NOMEM: return "out of memory";
+    default: return "unknown error";
+  }
+}
+
+int rs_init(rs_ctx** out, unsigned device_mask) {
+  if (!out) return RS_E_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RS_E_HIP;
+  auto ctx = std::make_unique<rs_ctx>();
+  for (int d = 0; d < count && d < 32; ++d) {
+    if (device_mask && !((device_mask >> d) & 1u)) continue;
+    auto dev = std::make_unique<Device>();
+    dev->id = d;
+    ctx->devs.push_back(std::move(dev));
+  }
+  if (ctx->devs.empty()) return RS_E_HIP;
+  *out = ctx.release();
+  return RS_OK;
+}
+
+void rs_shutdown(rs_ctx* ctx) { delete ctx; }
+
+int rs_device_count(const rs_ctx* ctx) { return ctx ? static_cast<int>(ctx->devs.size()) : 0; }
+
+int rs_shard_size(int k, int m, int64_t len, int64_t* shard_size) {
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!shard_size || len < 0) return RS_E_ARG;
+  if (len == 0) return RS_E_SHORT_DATA;
+  *shard_size = (len + k - 1) / k;
+  return RS_OK;
+}
+
+int rs_encode_matrix(int k, int m, uint8_t* out) {
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!out) return RS_E_ARG;
+  Mat E;
+  if (!encode_matrix(k, m, E)) return RS_E_SINGULAR;
+  std::memcpy(out, E.v.data(), E.v.size());
+  return RS_OK;
+}
+
+int rs_decode_rows(int k, int m, const uint8_t* present, int* valid_out, int* missing_out,
+                   int* n_missing, uint8_t* rows_out) {
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!present || !valid_out || !missing_out || !n_missing || !rows_out) return RS_E_ARG;
+  int np = 0;
+  for (int i = 0; i < k + m; ++i) np += present[i] != 0;
+  if (np < k) return RS_E_TOO_FEW_SHARDS;
+  DecodePlan dp;
+  if (!decode_plan(k, m, present, dp)) return RS_E_SINGULAR;
+  std::copy(dp.valid.begin(), dp.valid.end(), valid_out);
+  std::copy(dp.missing.begin(), dp.missing.end(), missing_out);
+  *n_missing = static_cast<int>(dp.missing.size());
+  std::memcpy(rows_out, dp.rows.v.data(), dp.missing.size() * static_cast<size_t>(k));
+  return RS_OK;
+}
+
+int rs_encode(rs_ctx* ctx, int k, int m, size_t S, const uint8_t* const* data,
+              uint8_t* const* parity) {
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!ctx || !data || !parity) return RS_E_ARG;
+  if (S == 0) return RS_E_NO_DATA;  // upstream Encode: checkShards -> ErrShardNoData
+  uint8_t present[256];
+  for (int i = 0; i < k + m; ++i) present[i] = i < k;
+  auto t = ctx->cache.get(k, m, present, false);
+  if (!t) return RS_E_SINGULAR;
+  return run_host(ctx, *t, S, [&](int i) { return data[i]; },
+                  [&](int i) { return parity[i - k]; });
+}
+
+int rs_codec_encode(rs_ctx* ctx, int k, int m, const uint8_t* data, size_t len,
+                    uint8_t* shards_out, size_t out_cap, size_t* shard_size) {
+  // codec.go:22-24 profile check, :26 New, :31 Split, :36 Encode
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!ctx || !shard_size || (len && (!data || !shards_out))) return RS_E_ARG;
+  if (len == 0) return RS_E_SHORT_DATA;
+  const size_t S = (len + k - 1) / k;
+  const int n = k + m;
+  if (out_cap < S * n) return RS_E_ARG;
+  if (shards_out != data) std::memmove(shards_out, data, len);
+  std::memset(shards_out + len, 0, S * k - len);  // Split zero padding
+  *shard_size = S;
+  uint8_t present[256];
+  for (int i = 0; i < n; ++i) present[i] = i < k;
+  auto t = ctx->cache.get(k, m, present, false);
+  if (!t) return RS_E_SINGULAR;
+  return run_host(ctx, *t, S, [&](int i) { return shards_out + S * i; },
+                  [&](int i) { return shards_out + S * i; });
+}
+
+int rs_reconstruct(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens) {
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!ctx || !shards || !lens) return RS_E_ARG;
+  return reconstruct_host(ctx, k, m, shards, lens, false);
+}
+
+int rs_verify(rs_ctx* ctx, int k, int m, const uint8_t* const* shards, const size_t* lens,
+              int* ok) {
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!ctx || !shards || !lens || !ok) return RS_E_ARG;
+  const int n = k + m;
+  size_t S = 0;
+  int np = 0;
+  if ((rc = check_lens(n, lens, false, &S, &np))) return rc;
+  uint8_t present[256];
+  for (int i = 0; i < n; ++i) present[i] = 1;
+  auto t = ctx->cache.get(k, m, present, true);
+  if (!t) return RS_E_SINGULAR;
+  rc = run_host(ctx, *t, S, [&](int i) { return shards[i]; },
+                [&](int) { return static_cast<uint8_t*>(nullptr); });
+  if (rc == RS_OK || rc == RS_E_CORRUPT) {
+    *ok = rc == RS_OK;
+    return RS_OK;
+  }
+  return rc;
+}
+
+int rs_codec_decode(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens,
+                    uint8_t* out, int64_t original_size) {
+  // codec.go:46-48 profile, :50 New, :55 Reconstruct, :59-65 Verify, :67-77 join/trim
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!ctx || !shards || !lens || original_size < 0 || (original_size && !out)) return RS_E_ARG;
+  rc = reconstruct_host(ctx, k, m, shards, lens, true);
+  if (rc) return rc;
+  const size_t S = lens[0];
+  if (static_cast<uint64_t>(S) * k < static_cast<uint64_t>(original_size))
+    return RS_E_INSUFFICIENT;
+  size_t left = static_cast<size_t>(original_size);
+  for (int i = 0; i < k && left; ++i) {
+    const size_t c = std::min(S, left);
+    std::memcpy(out + S * i, shards[i], c);
+    left -= c;
+  }
+  return RS_OK;
+}
+
+// ---- device-resident ----------------------------------------------------------------
+
+struct rs_plan {
+  int device = 0;
+  size_t S = 0;
+  int batch = 0;
+  bool aligned = true;
+  std::shared_ptr<const Tables> tables;
+  MetaLayout layout;
+  void* dmeta = nullptr;
+  uint64_t bytes = 0;
+};
+
+int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
+                   const uint8_t* present, uint8_t* const* shards, rs_plan** out) {
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!ctx || !shards || !out || batch < 1) return RS_E_ARG;
+  *out = nullptr;
+  Device* dev = ctx->device(device);
+  if (!dev) return RS_E_ARG;
+  const int n = k + m;
+  uint8_t pres[256];
+  int np = 0;
+  for (int i = 0; i < n; ++i) {
+    pres[i] = present ? (present[i] != 0) : (i < k);
+    np += pres[i];
+  }
+  if (np < k) return RS_E_TOO_FEW_SHARDS;
+  auto t = ctx->cache.get(k, m, pres, true);
+  if (!t) return RS_E_SINGULAR;
+  auto plan = std::make_unique<rs_plan>();
+  plan->device = device;
+  plan->S = S;
+  plan->batch = batch;
+  plan->tables = t;
+  plan->layout = meta_layout(*t, batch);
+  plan->bytes = algo_bytes(*t, S, batch);
+  std::vector<uint8_t> h(plan->layout.total);
+  plan->aligned = fill_meta(*t, plan->layout, batch, h.data(), [&](int b, int i) {
+    return static_cast<const uint8_t*>(shards[static_cast<size_t>(b) * n + i]);
+  });
+  HIPCHK(hipSetDevice(device));
+  if (hipMalloc(&plan->dmeta, plan->layout.total) != hipSuccess) return RS_E_NOMEM;
+  if (hipMemcpy(plan->dmeta, h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(plan->dmeta);
+    return RS_E_HIP;
+  }
+  *out = plan.release();
+  return RS_OK;
+}
+
+int rs_plan_launch(rs_plan* plan, void* stream) {
+  if (!plan) return RS_E_ARG;
+  HIPCHK(hipSetDevice(plan->device));
+  HIPCHK(launch_groups(*plan->tables, plan->layout, plan->batch,
+                       static_cast<uint8_t*>(plan->dmeta), plan->S, plan->aligned,
+                       static_cast<hipStream_t>(stream)));
+  return RS_OK;
+}
+
+int rs_plan_status(rs_plan* plan, void* stream, int* corrupt) {
+  if (!plan || !corrupt) return RS_E_ARG;
+  HIPCHK(hipSetDevice(plan->device));
+  auto s = static_cast<hipStream_t>(stream);
+  auto* st = static_cast<uint8_t*>(plan->dmeta) + plan->layout.status_off;
+  int v = 0;
+  HIPCHK(hipMemcpyAsync(&v, st, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemsetAsync(st, 0, sizeof(int), s));
+  HIPCHK(hipStreamSynchronize(s));
+  *corrupt = v != 0;
+  return RS_OK;
+}
+
+uint64_t rs_plan_bytes(const rs_plan* plan) { return plan ? plan->bytes : 0; }
+
+void rs_plan_destroy(rs_plan* plan) {
+  if (!plan) return;
+  (void)hipSetDevice(plan->device);
+  if (plan->dmeta) (void)hipFree(plan->dmeta);
+  delete plan;
+}
+
+static int one_shot(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
+                    const uint8_t* present, uint8_t* const* shards, void* stream) {
+  rs_plan* p = nullptr;
+  int rc = rs_plan_create(ctx, device, k, m, S, batch, present, shards, &p);
+  if (rc) return rc;
+  rc = rs_plan_launch(p, stream);
+  int corrupt = 0;
+  if (!rc) rc = rs_plan_status(p, stream, &corrupt);
+  rs_plan_destroy(p);
+  if (!rc && corrupt) rc = RS_E_CORRUPT;
+  return rc;
+}
+
+int rs_encode_dev(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
+                  uint8_t* const* shards, void* stream) {
+  return one_shot(ctx, device, k, m, S, batch, nullptr, shards, stream);
+}
+
+int rs_decode_dev(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
+                  const uint8_t* present, uint8_t* const* shards, void* stream) {
+  if (!present) return RS_E_ARG;
+  return one_shot(ctx, device, k, m, S, batch, present, shards, stream);
+}
+
+}  // extern "C"

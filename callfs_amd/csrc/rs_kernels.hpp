@@ -1,0 +1,34 @@
+// Launch interface of the GF(2^8) shard-matrix kernels (rs_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace callfs {
+
+constexpr int kMaxRowsPerLaunch = 8;  // output rows held in registers per launch
+constexpr int kMaxK = 256;
+
+// One launch applies an R x K coefficient block to every stripe of a batch:
+//   out[b][r][x] = XOR_i coef[r][i] * in[b][i][x]      for x in [0, S)
+// Rows with bit r of verify_mask set are compared against out[b][r] instead of
+// stored; any mismatch ORs 1 into *status (upstream Verify, codec.go:59).
+struct ApplyArgs {
+  const uint8_t* const* in_tab;  // [batch][K] device pointers (k valid shards)
+  uint8_t* const* out_tab;       // [batch][R] device pointers (written or compared)
+  const uint32_t* tabs;          // [K][R][5] v_perm tables (gf256.hpp perm_tables)
+  uint64_t S;                    // shard bytes
+  uint64_t nvec;                 // 16-byte vectors per shard handled by the vector kernel
+  uint32_t verify_mask;
+  int* status;
+  int K;
+  int R;
+  int batch;
+};
+
+// aligned: every in/out pointer is 16-byte aligned. Then [0, 16*floor(S/16)) runs on
+// the vector kernel and the ragged tail on the byte kernel; otherwise everything runs
+// on the byte kernel. Returns hipSuccess or the launch error.
+hipError_t launch_apply(ApplyArgs a, bool aligned, hipStream_t stream);
+
+}  // namespace callfs

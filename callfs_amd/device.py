@@ -1,0 +1,115 @@
+"""Device-resident stripes: plans over shards already in HBM.
+
+A *stripe* is one object's n = k+m shards. `StripeBatch` lays a batch of stripes out
+in one device allocation, `[batch][n][pitch]` bytes (pitch = S rounded up to 256 B so
+every shard starts 16-B aligned for the vector kernel), which is the layout the
+benchmark and the GPU tests use. `Plan` wraps rs_plan_create/rs_plan_launch: the
+coefficient tables and shard-pointer tables are uploaded once, and each launch only
+enqueues kernels on the given stream (capturable in a HIP graph).
+
+PyTorch is only the allocator and stream provider here; the arithmetic is the HIP
+kernels in libcallfs_rs.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import torch
+
+from . import _native as N
+
+
+def pitch_for(S: int) -> int:
+    return (S + 255) // 256 * 256
+
+
+class StripeBatch:
+    """`batch` stripes of RS(k, m) with shard size S, resident on `device`."""
+
+    def __init__(self, k: int, m: int, S: int, batch: int, device: torch.device):
+        self.k, self.m, self.S, self.batch = k, m, S, batch
+        self.n = k + m
+        self.pitch = pitch_for(S)
+        self.device = torch.device(device)
+        self.buf = torch.empty((batch, self.n, self.pitch), dtype=torch.uint8, device=self.device)
+
+    def shard(self, b: int, i: int) -> torch.Tensor:
+        return self.buf[b, i, : self.S]
+
+    def data(self) -> torch.Tensor:
+        return self.buf[:, : self.k, : self.S]
+
+    def parity(self) -> torch.Tensor:
+        return self.buf[:, self.k:, : self.S]
+
+    def pointers(self) -> list:
+        base = self.buf.data_ptr()
+        return [base + (b * self.n + i) * self.pitch for b in range(self.batch)
+                for i in range(self.n)]
+
+    def fill_random(self, seed: int) -> None:
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        self.buf.random_(0, 256, generator=g)
+
+
+class Plan:
+    """rs_plan over explicit device shard pointers (batch*n of them, stripe-major).
+
+    present=None is an encode plan (data present, parity missing); otherwise the
+    missing shards are reconstructed from the first k present ones and the remaining
+    present parity is re-verified (codec.go:55,59).
+    """
+
+    def __init__(self, k: int, m: int, S: int, batch: int, pointers: Sequence[int],
+                 present: Optional[Sequence[bool]] = None, device: int = 0,
+                 context: Optional[N.Context] = None):
+        self.ctx = context or N.default_context()
+        n = k + m
+        if len(pointers) != batch * n:
+            raise ValueError("need batch*(k+m) shard pointers")
+        self.k, self.m, self.S, self.batch, self.device = k, m, S, batch, device
+        ptrs = (ctypes.c_void_p * len(pointers))(*pointers)
+        pres = None
+        if present is not None:
+            if len(present) != n:
+                raise ValueError("present needs k+m flags")
+            pres = (ctypes.c_uint8 * n)(*[1 if p else 0 for p in present])
+        h = ctypes.c_void_p()
+        N.check(N.lib.rs_plan_create(self.ctx.handle, device, k, m, S, batch, pres, ptrs,
+                                     ctypes.byref(h)), "rs_plan_create")
+        self.handle = h
+
+    @classmethod
+    def for_batch(cls, sb: StripeBatch, present=None, context=None) -> "Plan":
+        dev = sb.device.index if sb.device.index is not None else 0
+        return cls(sb.k, sb.m, sb.S, sb.batch, sb.pointers(), present, dev, context)
+
+    @property
+    def bytes(self) -> int:
+        """Algorithmic HBM bytes one launch moves."""
+        return int(N.lib.rs_plan_bytes(self.handle))
+
+    def launch(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        N.check(N.lib.rs_plan_launch(self.handle, ctypes.c_void_p(s.cuda_stream)), "rs_plan_launch")
+
+    def corrupt(self, stream: Optional[torch.cuda.Stream] = None) -> bool:
+        """Synchronises the stream; True when a Verify row mismatched (then clears)."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        c = ctypes.c_int(0)
+        N.check(N.lib.rs_plan_status(self.handle, ctypes.c_void_p(s.cuda_stream),
+                                     ctypes.byref(c)), "rs_plan_status")
+        return bool(c.value)
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            N.lib.rs_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

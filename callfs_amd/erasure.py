@@ -1,0 +1,292 @@
+"""Host-side mirror of CallFS's Go `erasure` codec, backed by the HIP C ABI.
+
+Same names, argument meaning and error behaviour as the reference:
+
+    Go (erasure/)                                   here
+    ErasureProfile{DataShards,ParityShards,...}     ErasureProfile(data_shards, parity_shards, shard_size)  metadata.go:4-8
+    NewCodec()                                      Codec()                                                  codec.go:15-17
+    (*Codec).Encode(data, profile)                  Codec.encode(data, profile) -> list of n shards          codec.go:21-41
+    (*Codec).Decode(shards, profile, originalSize)  Codec.decode(shards, profile, original_size) -> bytes    codec.go:45-78
+    ShardChecksum(data)                             shard_checksum(data)                                     codec.go:81-84
+    ErrInsufficientShards/ErrShardCorrupted/...     exception classes of the same names                      errors.go:7-10
+
+Go compares the sentinel errors by identity (codec_test.go:113,118); here each
+sentinel is an exception class, and the wrapped upstream errors
+("erasure: failed to split data: %w", codec.go:33 …) are raised as instances of the
+upstream error's class carrying the wrapped message, so `isinstance` plays the role
+of errors.Is and str() matches the Go .Error() text.
+
+All shard arithmetic runs on the GPU through libcallfs_rs.so; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+
+# ---- errors (erasure/errors.go:7-10 and the upstream reedsolomon values) -------------
+
+class ErasureError(Exception):
+    """Base class for every error this module raises."""
+
+    text = "erasure error"
+
+    def __init__(self, message: Optional[str] = None):
+        super().__init__(message if message is not None else self.text)
+
+
+class ErrInsufficientShards(ErasureError):
+    text = "erasure: insufficient shards for reconstruction (code 3050)"
+
+
+class ErrShardCorrupted(ErasureError):
+    text = "erasure: shard checksum mismatch (code 3051)"
+
+
+class ErrInvalidProfile(ErasureError):
+    text = "erasure: invalid erasure profile parameters (code 3054)"
+
+
+class ErrShardNotFound(ErasureError):
+    text = "erasure: shard not found on this node (code 3055)"
+
+
+class ErrShortData(ErasureError):
+    text = "not enough data to fill the number of requested shards"
+
+
+class ErrTooFewShards(ErasureError):
+    text = "too few shards given"
+
+
+class ErrShardNoData(ErasureError):
+    text = "no shard data"
+
+
+class ErrShardSize(ErasureError):
+    text = "shard sizes do not match"
+
+
+class ErrSingular(ErasureError):
+    text = "matrix is singular"
+
+
+class ErrUnsupportedProfile(ErasureError):
+    """k+m > 256: upstream reedsolomon.New switches to Leopard GF(2^16); the GPU codec
+    does not implement it and the Go shim keeps the CPU codec for such profiles."""
+
+    text = "profile needs the GF(2^16) (Leopard) codec: k+m > 256"
+
+
+_UPSTREAM = {
+    N.RS_E_SHORT_DATA: ErrShortData,
+    N.RS_E_TOO_FEW_SHARDS: ErrTooFewShards,
+    N.RS_E_SHARD_SIZE: ErrShardSize,
+    N.RS_E_NO_DATA: ErrShardNoData,
+    N.RS_E_SINGULAR: ErrSingular,
+    N.RS_E_UNSUPPORTED: ErrUnsupportedProfile,
+}
+
+
+def _wrapped(rc: int, prefix: str) -> Exception:
+    """fmt.Errorf(prefix + ": %w", upstreamErr)."""
+    cls = _UPSTREAM.get(rc)
+    if cls is None:
+        return N.NativeError(rc, prefix)
+    return cls(f"{prefix}: {cls.text}")
+
+
+# ---- profile -----------------------------------------------------------------------
+
+@dataclass
+class ErasureProfile:
+    """erasure/metadata.go:4-8."""
+
+    data_shards: int
+    parity_shards: int
+    shard_size: int = 0
+
+
+def shard_checksum(data) -> str:
+    """codec.go:81-84: SHA-256 hex digest of a shard."""
+    return hashlib.sha256(bytes(data)).hexdigest()
+
+
+def _addr(buf) -> int:
+    """Address of a bytes-like object's first byte (read-only objects allowed)."""
+    a = np.frombuffer(buf, dtype=np.uint8)
+    return a.ctypes.data if a.size else 0
+
+
+def _writable(buf) -> bool:
+    return isinstance(buf, (bytearray, np.ndarray)) or (
+        isinstance(buf, memoryview) and not buf.readonly)
+
+
+class Codec:
+    """erasure/codec.go:12 Codec — stateless; one instance may be shared by threads
+    like the shared *Codec at erasure/manager.go:60."""
+
+    def __init__(self, context: Optional[N.Context] = None):
+        self._ctx = context
+
+    @property
+    def context(self) -> N.Context:
+        if self._ctx is None:
+            self._ctx = N.default_context()
+        return self._ctx
+
+    def encode(self, data, profile: ErasureProfile) -> List[memoryview]:
+        """codec.go:21-41. Returns data_shards+parity_shards equal-length shards (the
+        data is zero-padded to k*S, S = ceil(len/k)); they are views into one buffer,
+        the way upstream Split aliases the input."""
+        k, m = profile.data_shards, profile.parity_shards
+        if k < 1 or m < 1:
+            raise ErrInvalidProfile()
+        src = memoryview(data).cast("B") if not isinstance(data, (bytes, bytearray)) else data
+        L = len(src)
+        if L == 0:
+            raise ErrShortData(f"erasure: failed to split data: {ErrShortData.text}")
+        S = (L + k - 1) // k
+        out = bytearray(S * (k + m))
+        ss = ctypes.c_size_t(0)
+        rc = N.lib.rs_codec_encode(self.context.handle, k, m, _addr(src), L,
+                                   _addr(out), len(out), ctypes.byref(ss))
+        if rc == N.RS_E_INVALID_PROFILE:
+            raise ErrInvalidProfile()
+        if rc == N.RS_E_SHORT_DATA:
+            raise _wrapped(rc, "erasure: failed to split data")
+        if rc == N.RS_E_UNSUPPORTED:
+            raise _wrapped(rc, "erasure: failed to create encoder")
+        if rc != N.RS_OK:
+            raise _wrapped(rc, "erasure: failed to encode parity")
+        mv = memoryview(out)
+        return [mv[i * S:(i + 1) * S] for i in range(k + m)]
+
+    def decode(self, shards: List, profile: ErasureProfile, original_size: int) -> bytes:
+        """codec.go:45-78. `None` or empty entries are missing shards; they are
+        reconstructed in place (the list is mutated, as Go mutates its [][]byte)."""
+        k, m = profile.data_shards, profile.parity_shards
+        if k < 1 or m < 1:
+            raise ErrInvalidProfile()
+        n = k + m
+        if k + m > 256:
+            raise _wrapped(N.RS_E_UNSUPPORTED, "erasure: failed to create decoder")
+        if len(shards) != n:
+            raise ErrTooFewShards(f"erasure: reconstruction failed: {ErrTooFewShards.text}")
+        lens = (ctypes.c_size_t * n)()
+        for i, s in enumerate(shards):
+            lens[i] = 0 if s is None else len(s)
+        S = next((lens[i] for i in range(n) if lens[i]), 0)
+        bufs = list(shards)
+        for i in range(n):
+            if lens[i] == 0 and S:
+                bufs[i] = bytearray(S)  # upstream Reconstruct allocates missing shards
+        ptrs = (ctypes.c_void_p * n)(*[_addr(b) if b is not None and len(b) else 0
+                                      for b in bufs])
+        out = bytearray(max(int(original_size), 0))
+        rc = N.lib.rs_codec_decode(self.context.handle, k, m, ptrs, lens,
+                                   _addr(out) if out else None, int(original_size))
+        if rc in (N.RS_OK, N.RS_E_CORRUPT):
+            for i in range(n):
+                if shards[i] is None or len(shards[i]) == 0:
+                    shards[i] = bufs[i]
+        if rc == N.RS_OK:
+            return bytes(out)
+        if rc == N.RS_E_CORRUPT:
+            raise ErrShardCorrupted()
+        if rc == N.RS_E_INSUFFICIENT:
+            raise ErrInsufficientShards()
+        if rc == N.RS_E_INVALID_PROFILE:
+            raise ErrInvalidProfile()
+        if rc in (N.RS_E_TOO_FEW_SHARDS, N.RS_E_SHARD_SIZE, N.RS_E_NO_DATA, N.RS_E_SINGULAR):
+            raise _wrapped(rc, "erasure: reconstruction failed")
+        raise N.NativeError(rc, "erasure: decode")
+
+
+# ---- reedsolomon.Encoder-level helpers over host shards -----------------------------
+
+def _shard_ptrs(shards: Sequence) -> ctypes.Array:
+    return (ctypes.c_void_p * len(shards))(*[_addr(s) if s is not None and len(s) else 0
+                                             for s in shards])
+
+
+def encode_shards(shards: List, k: int, m: int, context: Optional[N.Context] = None) -> None:
+    """upstream enc.Encode(shards) (codec.go:36): fills shards[k:] in place. Parity
+    entries must be writable buffers of the data shards' size."""
+    ctx = context or N.default_context()
+    if len(shards) != k + m:
+        raise ErrTooFewShards()
+    S = len(shards[0])
+    if any(len(s) != S for s in shards):
+        raise ErrShardSize()
+    if not all(_writable(s) for s in shards[k:]):
+        raise TypeError("parity shards must be writable")
+    data = _shard_ptrs(shards[:k])
+    par = _shard_ptrs(shards[k:])
+    N.check(N.lib.rs_encode(ctx.handle, k, m, S, data, par), "rs_encode")
+
+
+def reconstruct(shards: List, k: int, m: int, context: Optional[N.Context] = None) -> None:
+    """upstream enc.Reconstruct(shards) (codec.go:55); missing entries are replaced."""
+    ctx = context or N.default_context()
+    n = k + m
+    if len(shards) != n:
+        raise ErrTooFewShards()
+    lens = (ctypes.c_size_t * n)(*[0 if s is None else len(s) for s in shards])
+    S = next((lens[i] for i in range(n) if lens[i]), 0)
+    bufs = [bytearray(S) if (lens[i] == 0 and S) else shards[i] for i in range(n)]
+    rc = N.lib.rs_reconstruct(ctx.handle, k, m, _shard_ptrs(bufs), lens)
+    if rc != N.RS_OK:
+        raise _wrapped(rc, "reconstruct")
+    for i in range(n):
+        if shards[i] is None or len(shards[i]) == 0:
+            shards[i] = bufs[i]
+
+
+def verify(shards: List, k: int, m: int, context: Optional[N.Context] = None) -> bool:
+    """upstream enc.Verify(shards) (codec.go:59)."""
+    ctx = context or N.default_context()
+    n = k + m
+    if len(shards) != n:
+        raise ErrTooFewShards()
+    lens = (ctypes.c_size_t * n)(*[0 if s is None else len(s) for s in shards])
+    ok = ctypes.c_int(0)
+    rc = N.lib.rs_verify(ctx.handle, k, m, _shard_ptrs(shards), lens, ctypes.byref(ok))
+    if rc != N.RS_OK:
+        raise _wrapped(rc, "verify")
+    return bool(ok.value)
+
+
+# ---- host-side matrices (no device needed) ------------------------------------------
+
+def encode_matrix(k: int, m: int) -> np.ndarray:
+    """(k+m) x k systematic matrix E = V . inv(V[0:k]) (upstream buildMatrix)."""
+    E = np.zeros((k + m, k), dtype=np.uint8)
+    rc = N.lib.rs_encode_matrix(k, m, E.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    if rc == N.RS_E_INVALID_PROFILE:
+        raise ErrInvalidProfile()
+    N.check(rc, "rs_encode_matrix")
+    return E
+
+
+def decode_rows(k: int, m: int, present: Sequence[bool]):
+    """(valid, missing, rows) as the fused decode kernel applies them."""
+    n = k + m
+    pr = np.array([1 if p else 0 for p in present], dtype=np.uint8)
+    valid = (ctypes.c_int * k)()
+    missing = (ctypes.c_int * n)()
+    nm = ctypes.c_int(0)
+    rows = np.zeros((n, k), dtype=np.uint8)
+    u8 = ctypes.POINTER(ctypes.c_uint8)
+    rc = N.lib.rs_decode_rows(k, m, pr.ctypes.data_as(u8), valid, missing, ctypes.byref(nm),
+                              rows.ctypes.data_as(u8))
+    if rc != N.RS_OK:
+        raise _wrapped(rc, "decode_rows")
+    return list(valid), list(missing)[:nm.value], rows[:nm.value]

@@ -1,0 +1,132 @@
+/*
+ * callfs_rs.h — C ABI of the MI355X-native Reed-Solomon erasure-coding path for CallFS.
+ *
+ * Drop-in boundary for erasure/codec.go: the Go package keeps its API
+ * (NewCodec/Encode/Decode, codec.go:15,21,45) and a cgo shim
+ * (erasure/codec_rocm.go, //go:build rocm && cgo — see INTEGRATION.md) binds the
+ * functions below. All GF(2^8) arithmetic that the reference delegates to
+ * github.com/klauspost/reedsolomon v1.13.3 (go.mod:13) runs here as hand-written
+ * HIP kernels for gfx950.
+ *
+ * Conventions
+ *  - Every function returns RS_OK (0) or a negative RS_E_* code.
+ *  - No pointer passed in is retained after return (cgo pointer rules).
+ *  - Host-memory entry points are synchronous (return after the D2H copy lands).
+ *  - All entry points are thread-safe; one rs_ctx may be shared by every request
+ *    goroutine, like the shared *Codec at erasure/manager.go:60.
+ *  - There is no CPU compute fallback: without a usable HIP device rs_init fails
+ *    with RS_E_HIP. Profiles with k+m > 256 (upstream switches to Leopard GF(2^16)
+ *    in reedsolomon.New, codec.go:26) return RS_E_UNSUPPORTED and the Go shim keeps
+ *    the CPU codec for them.
+ */
+#ifndef CALLFS_RS_H
+#define CALLFS_RS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RS_ABI_VERSION 1
+
+/* ---- error codes (mapped to Go errors by the shim) ---- */
+#define RS_OK                 0
+#define RS_E_INVALID_PROFILE (-1)  /* erasure.ErrInvalidProfile (errors.go:9; codec.go:22-24,46-48) */
+#define RS_E_SHORT_DATA      (-2)  /* reedsolomon.ErrShortData from Split (codec.go:31-34) */
+#define RS_E_TOO_FEW_SHARDS  (-3)  /* reedsolomon.ErrTooFewShards from Reconstruct (codec.go:55) */
+#define RS_E_SHARD_SIZE      (-4)  /* reedsolomon.ErrShardSize */
+#define RS_E_NO_DATA         (-5)  /* reedsolomon.ErrShardNoData */
+#define RS_E_CORRUPT         (-6)  /* erasure.ErrShardCorrupted (errors.go:8; codec.go:63-65) */
+#define RS_E_INSUFFICIENT    (-7)  /* erasure.ErrInsufficientShards (errors.go:7; codec.go:73-75) */
+#define RS_E_UNSUPPORTED     (-8)  /* k+m > 256: Leopard GF(2^16) path, not implemented on GPU */
+#define RS_E_HIP             (-9)  /* HIP runtime failure / no device */
+#define RS_E_ARG             (-10) /* NULL pointer, short buffer, bad count */
+#define RS_E_SINGULAR        (-11) /* reedsolomon.ErrSingular (cannot happen for valid profiles) */
+#define RS_E_NOMEM           (-12) /* host or device allocation failed */
+
+typedef struct rs_ctx rs_ctx;
+typedef struct rs_plan rs_plan;
+
+/* ---- lifetime ---------------------------------------------------------------------
+ * Replaces NewCodec (erasure/codec.go:15-17). device_mask: bit d selects HIP device d;
+ * 0 selects every visible device. Host-memory calls are spread over the selected
+ * devices (one per call, round-robin). */
+int  rs_init(rs_ctx** out, unsigned device_mask);
+void rs_shutdown(rs_ctx* ctx);
+int  rs_device_count(const rs_ctx* ctx);
+int  rs_abi_version(void);
+const char* rs_strerror(int code);
+
+/* ---- host-side helpers (no device needed) -------------------------------------------
+ * rs_shard_size: S = ceil(len/k) as upstream Split computes it (codec.go:31).
+ * rs_encode_matrix: E = V . inv(V[0:k]), (k+m) x k row-major (upstream buildMatrix,
+ *   reached via reedsolomon.New at codec.go:26).
+ * rs_decode_rows: for a presence mask over n = k+m shards, the first k present
+ *   indices (valid), the missing indices, and the rows over the valid shards that
+ *   produce every missing shard (data rows of inv(E[valid]); parity rows
+ *   P[j].inv(E[valid])), as upstream Reconstruct computes them (codec.go:55).
+ *   valid_out: k ints; missing_out: n ints; rows_out: n*k bytes (n_missing*k used). */
+int rs_shard_size(int k, int m, int64_t len, int64_t* shard_size);
+int rs_encode_matrix(int k, int m, uint8_t* out);
+int rs_decode_rows(int k, int m, const uint8_t* present, int* valid_out, int* missing_out,
+                   int* n_missing, uint8_t* rows_out);
+
+/* ---- Codec-level, host memory (the cgo shim's two calls) ----------------------------
+ * rs_codec_encode replaces Codec.Encode (erasure/codec.go:21-41): Split + Encode.
+ *   Writes n = k+m shards of S = ceil(len/k) bytes back to back into shards_out
+ *   (shard i at offset i*S; needs out_cap >= n*S). *shard_size receives S.
+ *   len == 0 -> RS_E_SHORT_DATA (upstream Split).
+ * rs_codec_decode replaces Codec.Decode (erasure/codec.go:45-78): Reconstruct + Verify
+ *   + join + trim. shards[i] points to a buffer of at least S bytes for every i;
+ *   lens[i] is that shard's length, 0 meaning missing (nil in Go). Missing shards are
+ *   reconstructed INTO shards[i] and lens[i] is set to S (Decode mutates its shards
+ *   argument in Go). out receives original_size bytes.
+ *   Error precedence follows codec.go: profile, shard count/size, too few, corrupt,
+ *   insufficient. */
+int rs_codec_encode(rs_ctx* ctx, int k, int m, const uint8_t* data, size_t len,
+                    uint8_t* shards_out, size_t out_cap, size_t* shard_size);
+int rs_codec_decode(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens,
+                    uint8_t* out, int64_t original_size);
+
+/* ---- Encoder-level, host memory (reedsolomon.Encoder methods used by codec.go) -----
+ * rs_encode:      enc.Encode(shards)      (codec.go:36)  data: k ptrs, parity: m ptrs, S bytes each
+ * rs_reconstruct: enc.Reconstruct(shards) (codec.go:55)  same buffer/lens contract as rs_codec_decode
+ * rs_verify:      enc.Verify(shards)      (codec.go:59)  *ok = 1 when parity matches */
+int rs_encode(rs_ctx* ctx, int k, int m, size_t S, const uint8_t* const* data,
+              uint8_t* const* parity);
+int rs_reconstruct(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens);
+int rs_verify(rs_ctx* ctx, int k, int m, const uint8_t* const* shards, const size_t* lens,
+              int* ok);
+
+/* ---- device-resident plans (batched stripes, graph-capturable launches) -------------
+ * A plan fixes (k, m, S, batch, presence mask) and the device pointers of every
+ * stripe's n shards: shards[b*n + i] is shard i of stripe b (device memory, S bytes).
+ * present == NULL means "encode" (data present, parity missing). Launching a plan
+ * computes every missing shard of every stripe from the first k present ones and
+ * re-checks the remaining present parity (the Verify of codec.go:59), OR-ing 1 into
+ * the plan's device status word on mismatch. rs_plan_launch only enqueues work on
+ * `stream` (a hipStream_t; NULL = the null stream) — no allocation, no sync.
+ * rs_plan_status synchronises `stream`, returns the status word in *corrupt and
+ * clears it. rs_plan_bytes: algorithmic HBM bytes one launch moves
+ * (reads of the k+verify inputs + writes of the missing shards). */
+int  rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
+                    const uint8_t* present, uint8_t* const* shards, rs_plan** out);
+int  rs_plan_launch(rs_plan* plan, void* stream);
+int  rs_plan_status(rs_plan* plan, void* stream, int* corrupt);
+uint64_t rs_plan_bytes(const rs_plan* plan);
+void rs_plan_destroy(rs_plan* plan);
+
+/* One-shot device-resident calls (build + launch + free; tables cached per profile).
+ * Same pointer layout as rs_plan_create; synchronous on `stream`. rs_decode_dev
+ * returns RS_E_CORRUPT when the verify rows mismatch. */
+int rs_encode_dev(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
+                  uint8_t* const* shards, void* stream);
+int rs_decode_dev(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
+                  const uint8_t* present, uint8_t* const* shards, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CALLFS_RS_H */

@@ -1,0 +1,88 @@
+"""The C ABI library without a GPU: it loads, exports every symbol include/callfs_rs.h
+declares, and its host-side matrix logic matches the oracle. No kernel launches."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import rs_oracle as o
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "callfs_rs.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rs_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_exports_every_declared_symbol(native_lib):
+    names = header_functions()
+    assert len(names) >= 19
+    for name in names:
+        assert hasattr(native_lib.lib, name), name
+    assert set(names) == set(native_lib.SIGNATURES), "ctypes table out of sync with header"
+
+
+def test_abi_version(native_lib):
+    assert native_lib.lib.rs_abi_version() == 1
+
+
+def test_error_strings_match_reference(native_lib):
+    s = native_lib.strerror
+    assert s(native_lib.RS_E_INVALID_PROFILE) == "erasure: invalid erasure profile parameters (code 3054)"
+    assert s(native_lib.RS_E_CORRUPT) == "erasure: shard checksum mismatch (code 3051)"
+    assert s(native_lib.RS_E_INSUFFICIENT) == "erasure: insufficient shards for reconstruction (code 3050)"
+    assert s(native_lib.RS_E_SHORT_DATA) == "not enough data to fill the number of requested shards"
+    assert s(native_lib.RS_E_TOO_FEW_SHARDS) == "too few shards given"
+
+
+@pytest.mark.parametrize("k,m", [(1, 1), (2, 1), (3, 2), (4, 2), (10, 4), (16, 4), (5, 5),
+                                 (20, 12), (128, 128), (255, 1)])
+def test_encode_matrix_matches_oracle(native_lib, k, m):
+    from callfs_amd.erasure import encode_matrix
+    assert encode_matrix(k, m).tolist() == o.encode_matrix(k, m)
+
+
+def test_encode_matrix_kat_rows(native_lib):
+    from callfs_amd.erasure import encode_matrix
+    for (k, m), rows in o.KATS["parity_rows"].items():
+        assert encode_matrix(k, m)[k:].tolist() == rows
+
+
+@pytest.mark.parametrize("erase", [(0, 1, 2, 3), (0, 3, 7, 12), (10, 11, 12, 13), (9,), (13,)])
+def test_decode_rows_match_oracle(native_lib, erase):
+    from callfs_amd.erasure import decode_rows
+    k, m = 10, 4
+    present = [i not in erase for i in range(k + m)]
+    valid, missing, rows = decode_rows(k, m, present)
+    ov, om, orows = o.decode_rows(k, m, present)
+    assert valid == ov and missing == om and rows.tolist() == orows
+
+
+def test_profile_errors_without_device(native_lib):
+    from callfs_amd import erasure as E
+    with pytest.raises(E.ErrInvalidProfile):
+        E.encode_matrix(0, 2)
+    with pytest.raises(E.ErrInvalidProfile):
+        E.encode_matrix(4, 0)
+    ss = ctypes.c_int64(0)
+    assert native_lib.lib.rs_shard_size(10, 4, 64 << 20, ctypes.byref(ss)) == 0
+    assert ss.value == 6710887  # RS(10,4) on 64 MiB
+    assert native_lib.lib.rs_shard_size(10, 4, 1 << 30, ctypes.byref(ss)) == 0
+    assert ss.value == 107374183
+    assert native_lib.lib.rs_shard_size(4, 2, 0, ctypes.byref(ss)) == native_lib.RS_E_SHORT_DATA
+    assert native_lib.lib.rs_shard_size(200, 57, 10, ctypes.byref(ss)) == native_lib.RS_E_UNSUPPORTED
+
+
+def test_init_fails_loudly_without_gpu(native_lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    h = ctypes.c_void_p()
+    assert native_lib.lib.rs_init(ctypes.byref(h), 0) == native_lib.RS_E_HIP
+    with pytest.raises(RuntimeError):
+        native_lib.Context()
