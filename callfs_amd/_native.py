@@ -18,6 +18,15 @@ if not os.path.exists(LIB_PATH):
         f"{LIB_PATH} is missing: build it with `python -m callfs_amd.build` "
         "(hipcc --offload-arch=gfx950); the RS path has no CPU fallback")
 
+# PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7, loaded by file
+# name). Loading torch first lets our DT_NEEDED libamdhip64.so.7 bind to that copy, so
+# the process has ONE HIP/HSA runtime; loading ours first would bring in /opt/rocm's
+# copy beside torch's and the second runtime fails to initialise the device.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - plain C-ABI use without torch
+    pass
+
 lib = ctypes.CDLL(LIB_PATH)
 
 RS_OK = 0
