@@ -1,0 +1,265 @@
+// Device code of the GF(2^8) shard-matrix kernels for gfx950 (MI355X, CDNA4).
+//
+// Replaces the SIMD kernels of github.com/klauspost/reedsolomon v1.13.3 (go.mod:13)
+// behind erasure/codec.go:36 (Encode), :55 (Reconstruct) and :59 (Verify).
+//
+// Design (DESIGN.md "Kernels"):
+//  * Byte-wise integer work, HBM-bound: no MFMA, no LDS. Each lane owns U 16-byte
+//    column vectors of a stripe and streams them through all K input shards with
+//    global_load_dwordx4, keeping the R output vectors in registers, then writes (or,
+//    for Verify rows, compares) them once: (K + R) * 16 bytes of compulsory HBM
+//    traffic per vector, nothing re-read (confirmed by rocprofv3 FETCH/WRITE_SIZE).
+//  * GF multiply by a wave-uniform coefficient c on 4 packed bytes = three v_perm_b32
+//    byte-selects from 8-byte tables: c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6]
+//    (gf256.hpp perm_tables). The three selectors depend only on the data word, so
+//    they are shared by all R rows; per row and data word the cost is 3 v_perm plus
+//    1.5 v_bitop3 (three-input XOR, gfx950). Tables and shard pointers are read
+//    through the constant address space, so they arrive by s_load in SGPRs: no LDS,
+//    no bank conflicts on random data, no per-lane table registers.
+//  * Input shards are consumed in pairs with the next pair's loads in flight, so
+//    register use does not grow with K (62 VGPRs at K=10, R=4: 8 waves/SIMD).
+//  * Ragged tails (S % 16) and unaligned shard pointers take the byte kernel.
+#pragma once
+
+#include "rs_kernels.hpp"
+
+namespace callfs {
+namespace dev {
+
+constexpr int kBlock = 256;
+
+template <class T>
+using cptr = const __attribute__((address_space(4))) T*;
+
+template <class T>
+__device__ __forceinline__ cptr<T> as_const(const T* p) {
+  return (cptr<T>)(p);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
+}
+
+struct Sel {
+  uint32_t i0, i1, i2;
+};
+
+__device__ __forceinline__ Sel selectors(uint32_t x) {
+  return Sel{x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
+}
+
+// c*x for 4 packed bytes, as three partial products (XOR them to finish).
+struct Prod {
+  uint32_t p0, p1, p2;
+};
+
+__device__ __forceinline__ Prod gf_mul4(const Sel& s, cptr<uint32_t> t) {
+  return Prod{__builtin_amdgcn_perm(t[1], t[0], s.i0), __builtin_amdgcn_perm(t[3], t[2], s.i1),
+              __builtin_amdgcn_perm(t[4], t[4], s.i2)};
+}
+
+// acc ^ a ^ b with three v_bitop3 for the six partial products.
+__device__ __forceinline__ uint32_t fma2(uint32_t acc, const Prod& a, const Prod& b) {
+  acc = xor3(acc, a.p0, a.p1);
+  acc = xor3(acc, a.p2, b.p0);
+  return xor3(acc, b.p1, b.p2);
+}
+
+__device__ __forceinline__ uint32_t fma1(uint32_t acc, const Prod& a) {
+  return xor3(acc, a.p0, xor3(a.p1, a.p2, 0u));
+}
+
+__device__ __forceinline__ uint32_t word(const uint4& v, int w) {
+  return w == 0 ? v.x : (w == 1 ? v.y : (w == 2 ? v.z : v.w));
+}
+
+// Compile-time launch policy of the vector kernel.
+//   WPE      minimum waves per SIMD the register allocation must allow
+//   U        16-B column vectors per lane (tile = 256*U vectors of a stripe)
+//   NT_LOAD  / NT_STORE: non-temporal (streaming) global loads / stores
+//   PERSIST  grid-stride over tiles with a fixed grid instead of one tile per block
+template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_>
+struct Policy {
+  static constexpr int WPE = WPE_;
+  static constexpr int U = U_;
+  static constexpr bool NT_LOAD = NT_LOAD_;
+  static constexpr bool NT_STORE = NT_STORE_;
+  static constexpr bool PERSIST = PERSIST_;
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <class P>
+__device__ __forceinline__ uint4 load16(const uint4* p) {
+  if constexpr (P::NT_LOAD) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *p;
+  }
+}
+
+template <class P>
+__device__ __forceinline__ void store16(uint4* p, const uint4& v) {
+  if constexpr (P::NT_STORE) {
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+  } else {
+    *p = v;
+  }
+}
+
+template <int RT, int U>
+__device__ __forceinline__ void mac_pair(uint32_t (&acc)[U][RT][4], const uint4 (&xa)[U],
+                                         const uint4 (&xb)[U], cptr<uint32_t> ta,
+                                         cptr<uint32_t> tb) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const Sel sa = selectors(word(xa[u], w)), sb = selectors(word(xb[u], w));
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+        acc[u][r][w] = fma2(acc[u][r][w], gf_mul4(sa, ta + r * 5), gf_mul4(sb, tb + r * 5));
+    }
+}
+
+template <int RT, int U>
+__device__ __forceinline__ void mac_one(uint32_t (&acc)[U][RT][4], const uint4 (&xa)[U],
+                                        cptr<uint32_t> ta) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const Sel sa = selectors(word(xa[u], w));
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[u][r][w] = fma1(acc[u][r][w], gf_mul4(sa, ta + r * 5));
+    }
+}
+
+// Tiles: a stripe's nvec vectors are cut into tiles of 256*U; tile t covers stripe
+// t / tiles_per_stripe. Every tile is wave-uniform in its stripe, so shard pointers
+// stay scalar.
+template <int KT, int RT, class P>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P::WPE, 8)))
+void rs_apply_vec(ApplyArgs a) {
+  constexpr int U = P::U;
+  const int K = KT ? KT : a.K;
+  const int npairs = K >> 1;
+  const uint32_t tile_vecs = kBlock * U;
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + tile_vecs - 1) / tile_vecs);
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
+  const cptr<uint32_t> tabs = as_const(a.tabs);
+
+  for (uint32_t t = blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
+    const uint32_t stripe = t / tps;
+    const uint64_t v0 = static_cast<uint64_t>(t - stripe * tps) * tile_vecs + threadIdx.x;
+    cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
+    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * RT;
+    bool live[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) live[u] = v0 + static_cast<uint64_t>(u) * kBlock < a.nvec;
+    if (!live[0]) continue;
+
+    auto ld = [&](int i, uint4 (&x)[U]) {
+      const uint4* src = reinterpret_cast<const uint4*>(in[i]) + v0;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        x[u] = (u == 0 || live[u]) ? load16<P>(src + u * kBlock) : make_uint4(0, 0, 0, 0);
+    };
+
+    uint32_t acc[U][RT][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) acc[u][r][w] = 0;
+
+    uint4 xa[U], xb[U];
+    if (npairs) {
+      ld(0, xa);
+      ld(1, xb);
+    }
+#pragma unroll 1
+    for (int p = 0; p < npairs; ++p) {
+      uint4 ya[U], yb[U];
+      if (p + 1 < npairs) {
+        ld(2 * p + 2, ya);
+        ld(2 * p + 3, yb);
+      }
+      const cptr<uint32_t> ta = tabs + static_cast<size_t>(2 * p) * RT * 5;
+      mac_pair<RT, U>(acc, xa, xb, ta, ta + RT * 5);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        xa[u] = ya[u];
+        xb[u] = yb[u];
+      }
+    }
+    if (K & 1) {
+      ld(K - 1, xa);
+      mac_one<RT, U>(acc, xa, tabs + static_cast<size_t>(K - 1) * RT * 5);
+    }
+
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      uint4* dst = reinterpret_cast<uint4*>(out[r]) + v0;
+      const bool cmp = (a.verify_mask >> r) & 1u;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!live[u]) continue;
+        const uint4 o = make_uint4(acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]);
+        if (cmp) {
+          const uint4 y = dst[u * kBlock];
+          bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) != 0;
+        } else {
+          store16<P>(dst + u * kBlock, o);
+        }
+      }
+    }
+    if (bad) atomicOr(a.status, 1);
+  }
+}
+
+// One byte position per lane over [b0, S): ragged tails and unaligned pointers.
+template <int RT>
+__global__ __launch_bounds__(kBlock) void rs_apply_bytes(ApplyArgs a, uint64_t b0) {
+  const uint64_t b = b0 + static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (b >= a.S) return;
+  const cptr<uint32_t> tabs = as_const(a.tabs);
+  for (int stripe = blockIdx.y; stripe < a.batch; stripe += gridDim.y) {
+    cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * a.K;
+    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * RT;
+    uint32_t acc[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r] = 0;
+    for (int i = 0; i < a.K; ++i) {
+      const Sel s = selectors(in[i][b]);
+      const cptr<uint32_t> t = tabs + static_cast<size_t>(i) * RT * 5;
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[r] = fma1(acc[r], gf_mul4(s, t + r * 5));
+    }
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const uint8_t v = static_cast<uint8_t>(acc[r]);
+      if ((a.verify_mask >> r) & 1u) bad |= out[r][b] != v;
+      else out[r][b] = v;
+    }
+    if (bad) atomicOr(a.status, 1);
+  }
+}
+
+// Grid for the vector kernel: one tile per block, or (PERSIST) a fixed grid of
+// `blocks_per_cu` blocks on each of the 256 CUs.
+template <class P>
+inline unsigned vec_grid(uint64_t nvec, int batch, int blocks_per_cu = 8) {
+  const uint64_t tile = static_cast<uint64_t>(kBlock) * P::U;
+  const uint64_t ntiles = (nvec + tile - 1) / tile * static_cast<uint64_t>(batch);
+  if (P::PERSIST) return static_cast<unsigned>(std::min<uint64_t>(ntiles, 256ull * blocks_per_cu));
+  return static_cast<unsigned>(ntiles);
+}
+
+}  // namespace dev
+}  // namespace callfs

@@ -1,0 +1,218 @@
+// Kernel A/B harness for the RS vector kernel (development tool, not product).
+//
+// Interleaves every variant in one process (cdna_hip_programming.md §5.4 rule 24):
+// R rounds x V variants, each timed with hipEvents over ITERS back-to-back launches on
+// one stream, on a device-resident batch far larger than the 256 MiB MALL. Every
+// variant's parity is compared with the production policy's (bit-exact). Also times
+// an XOR-only kernel with the identical access pattern (K loads + R stores per 16-B
+// vector, no GF work) as the memory ceiling of this traffic shape, and hipMemcpy D2D.
+//
+// build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I callfs_amd/csrc tools/kbench.hip -o tools/kbench
+// run:   tools/kbench [k m shard_bytes stripes rounds iters]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "gf256.hpp"
+#include "rs_apply.hpp"
+
+using namespace callfs;
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,            \
+                   hipGetErrorString(e_));                                      \
+      std::exit(1);                                                             \
+    }                                                                           \
+  } while (0)
+
+__global__ void fill_kernel(uint32_t* p, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t x = static_cast<uint32_t>(i) * 0x9E3779B1u ^ seed ^ static_cast<uint32_t>(i >> 32);
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    p[i] = x;
+  }
+}
+
+// Memory ceiling for this traffic shape: K 16-B loads, R 16-B stores per lane.
+template <int K, int R, bool NT>
+__global__ __launch_bounds__(256) void xor_stream(ApplyArgs a) {
+  using P = dev::Policy<4, 1, NT, NT, false>;
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + 255) / 256);
+  const uint32_t t = blockIdx.x;
+  const uint32_t stripe = t / tps;
+  const uint64_t v = static_cast<uint64_t>(t - stripe * tps) * 256 + threadIdx.x;
+  if (v >= a.nvec) return;
+  dev::cptr<const uint8_t*> in = dev::as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
+  dev::cptr<uint8_t*> out = dev::as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
+  uint4 x[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) x[i] = dev::load16<P>(reinterpret_cast<const uint4*>(in[i]) + v);
+  uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    acc.x ^= x[i].x; acc.y ^= x[i].y; acc.z ^= x[i].z; acc.w ^= x[i].w;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    dev::store16<P>(reinterpret_cast<uint4*>(out[r]) + v, make_uint4(acc.x + r, acc.y, acc.z, acc.w));
+}
+
+struct Variant {
+  std::string name;
+  std::function<void(const ApplyArgs&, hipStream_t)> launch;
+  bool check = true;
+};
+
+template <int K, int R, class P>
+Variant make_variant(const char* name, int blocks_per_cu = 8) {
+  return Variant{name, [blocks_per_cu](const ApplyArgs& a, hipStream_t s) {
+                   const unsigned g = dev::vec_grid<P>(a.nvec, a.batch, blocks_per_cu);
+                   hipLaunchKernelGGL((dev::rs_apply_vec<K, R, P>), dim3(g), dim3(256), 0, s, a);
+                 }};
+}
+
+int main(int argc, char** argv) {
+  const int k = argc > 1 ? std::atoi(argv[1]) : 10;
+  const int m = argc > 2 ? std::atoi(argv[2]) : 4;
+  const size_t S = argc > 3 ? std::strtoull(argv[3], nullptr, 0) : (1u << 20);
+  const int B = argc > 4 ? std::atoi(argv[4]) : 256;
+  const int rounds = argc > 5 ? std::atoi(argv[5]) : 5;
+  const int iters = argc > 6 ? std::atoi(argv[6]) : 10;
+  if (k != 10 || m != 4) {
+    std::fprintf(stderr, "variants are instantiated for k=10 m=4\n");
+    return 2;
+  }
+  const int n = k + m;
+  const size_t pitch = (S + 255) / 256 * 256;
+  const size_t total = pitch * n * B;
+  uint8_t* buf;
+  CK(hipMalloc(&buf, total));
+  hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint32_t*>(buf),
+                     total / 4, 12345u);
+  uint8_t* ref;  // parity of the production variant
+  CK(hipMalloc(&ref, pitch * m * B));
+
+  // tables (encode: parity rows of E)
+  Mat E;
+  encode_matrix(k, m, E);
+  std::vector<uint32_t> tabs(static_cast<size_t>(k) * m * 5);
+  for (int i = 0; i < k; ++i)
+    for (int r = 0; r < m; ++r) perm_tables(E.at(k + r, i), &tabs[(static_cast<size_t>(i) * m + r) * 5]);
+  std::vector<const uint8_t*> in(static_cast<size_t>(B) * k);
+  std::vector<uint8_t*> out(static_cast<size_t>(B) * m);
+  for (int b = 0; b < B; ++b) {
+    for (int i = 0; i < k; ++i) in[b * k + i] = buf + (static_cast<size_t>(b) * n + i) * pitch;
+    for (int r = 0; r < m; ++r) out[b * m + r] = buf + (static_cast<size_t>(b) * n + k + r) * pitch;
+  }
+  void *d_in, *d_out, *d_tabs;
+  int* d_status;
+  CK(hipMalloc(&d_in, in.size() * sizeof(void*)));
+  CK(hipMalloc(&d_out, out.size() * sizeof(void*)));
+  CK(hipMalloc(&d_tabs, tabs.size() * 4));
+  CK(hipMalloc(&d_status, 4));
+  CK(hipMemcpy(d_in, in.data(), in.size() * sizeof(void*), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_out, out.data(), out.size() * sizeof(void*), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemset(d_status, 0, 4));
+
+  ApplyArgs a{};
+  a.in_tab = static_cast<const uint8_t* const*>(d_in);
+  a.out_tab = static_cast<uint8_t* const*>(d_out);
+  a.tabs = static_cast<const uint32_t*>(d_tabs);
+  a.S = S;
+  a.nvec = S / 16;
+  a.verify_mask = 0;
+  a.status = d_status;
+  a.K = k;
+  a.R = m;
+  a.batch = B;
+
+  using namespace dev;
+  std::vector<Variant> vs;
+  vs.push_back(make_variant<10, 4, Policy<4, 1, false, false, false>>("prod wpe4 u1"));
+  vs.push_back(make_variant<10, 4, Policy<4, 1, true, true, false>>("nt wpe4 u1"));
+  vs.push_back(make_variant<10, 4, Policy<8, 1, true, true, false>>("nt wpe8 u1"));
+  vs.push_back(make_variant<10, 4, Policy<4, 2, true, true, false>>("nt wpe4 u2"));
+  vs.push_back(make_variant<0, 4, Policy<4, 1, false, false, false>>("rtK wpe4"));
+  vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, false>>("rtK nt wpe4"));
+  vs.push_back(make_variant<0, 4, Policy<8, 1, true, true, false>>("rtK nt wpe8"));
+  vs.push_back(make_variant<0, 4, Policy<4, 2, true, true, false>>("rtK nt u2"));
+  vs.push_back(make_variant<0, 4, Policy<2, 2, true, true, false>>("rtK nt u2 wpe2"));
+  vs.push_back(Variant{"xor-stream (ceiling)", [](const ApplyArgs& a, hipStream_t s) {
+                         const unsigned g = static_cast<unsigned>((a.nvec + 255) / 256 * a.batch);
+                         hipLaunchKernelGGL((xor_stream<10, 4, false>), dim3(g), dim3(256), 0, s, a);
+                       }, false});
+  vs.push_back(Variant{"xor-stream nt (ceiling)", [](const ApplyArgs& a, hipStream_t s) {
+                         const unsigned g = static_cast<unsigned>((a.nvec + 255) / 256 * a.batch);
+                         hipLaunchKernelGGL((xor_stream<10, 4, true>), dim3(g), dim3(256), 0, s, a);
+                       }, false});
+  vs.push_back(Variant{"hipMemcpy D2D same bytes/2", [&](const ApplyArgs&, hipStream_t s) {
+                         // read+write of (k+m)/2*S per stripe: same total bytes moved
+                         const size_t half = static_cast<size_t>(B) * n * pitch / 2;
+                         CK(hipMemcpyAsync(buf + half, buf, half, hipMemcpyDeviceToDevice, s));
+                       }, false});
+
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  // production reference parity
+  vs[0].launch(a, s);
+  CK(hipStreamSynchronize(s));
+  CK(hipGetLastError());
+  for (int b = 0; b < B; ++b)
+    CK(hipMemcpy(ref + static_cast<size_t>(b) * m * pitch, out[b * m], m * pitch, hipMemcpyDeviceToDevice));
+
+  const double bytes = static_cast<double>(B) * S * n;
+  std::vector<std::vector<double>> ms(vs.size());
+  std::vector<uint8_t> h1(m * pitch), h2(m * pitch);
+  for (int rd = 0; rd < rounds; ++rd) {
+    for (size_t vi = 0; vi < vs.size(); ++vi) {
+      vs[vi].launch(a, s);  // warm
+      CK(hipEventRecord(e0, s));
+      for (int it = 0; it < iters; ++it) vs[vi].launch(a, s);
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      CK(hipGetLastError());
+      float t = 0;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      ms[vi].push_back(t / iters);
+      if (rd == 0 && vs[vi].check) {
+        for (int b : {0, B / 2, B - 1}) {
+          CK(hipMemcpy(h1.data(), ref + static_cast<size_t>(b) * m * pitch, m * pitch, hipMemcpyDeviceToHost));
+          CK(hipMemcpy(h2.data(), out[b * m], m * pitch, hipMemcpyDeviceToHost));
+          bool same = true;
+          for (int r = 0; r < m; ++r) same &= !std::memcmp(&h1[r * pitch], &h2[r * pitch], S);
+          if (!same) std::printf("MISMATCH variant %s stripe %d\n", vs[vi].name.c_str(), b);
+        }
+      }
+      if (!vs[vi].check) {  // restore parity clobbered by ceiling kernels
+        for (int b = 0; b < B; ++b)
+          CK(hipMemcpy(out[b * m], ref + static_cast<size_t>(b) * m * pitch, m * pitch, hipMemcpyDeviceToDevice));
+      }
+    }
+  }
+  std::printf("RS(%d,%d) S=%zu stripes=%d  working set %.2f GiB  rounds=%d iters=%d\n", k, m, S, B,
+              total / 1073741824.0, rounds, iters);
+  std::printf("%-28s %10s %10s %10s %8s\n", "variant", "med_us", "min_us", "GB/s(med)", "%8TB/s");
+  for (size_t vi = 0; vi < vs.size(); ++vi) {
+    auto v = ms[vi];
+    std::sort(v.begin(), v.end());
+    const double med = v[v.size() / 2], mn = v[0];
+    const double gbs = bytes / (med * 1e-3) / 1e9;
+    std::printf("%-28s %10.1f %10.1f %10.1f %8.1f\n", vs[vi].name.c_str(), med * 1e3, mn * 1e3, gbs,
+                gbs / 80.0);
+  }
+  return 0;
+}
