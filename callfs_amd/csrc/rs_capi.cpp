@@ -17,11 +17,13 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
-#include <list>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -122,6 +124,102 @@ class TableCache {
   std::unordered_map<std::string, std::shared_ptr<const Tables>> map_;
 };
 
+// ---- host copy pool ---------------------------------------------------------------
+
+// Parallel memcpy for pageable <-> pinned staging. A job's segments are cut into
+// pieces; the calling thread and the pool's workers take pieces until none are left.
+// Threads: CALLFS_RS_COPY_THREADS, default min(8, hardware threads).
+class CopyPool {
+ public:
+  struct Seg {
+    void* dst;
+    const void* src;
+    size_t n;
+  };
+
+  CopyPool() {
+    int n = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = std::getenv("CALLFS_RS_COPY_THREADS")) n = std::max(1, std::atoi(e));
+    for (int i = 1; i < n; ++i) workers_.emplace_back([this] { loop(); });
+  }
+
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+  void run(const std::vector<Seg>& segs) {
+    size_t total = 0;
+    for (const Seg& s : segs) total += s.n;
+    if (workers_.empty() || total < kInline) {
+      for (const Seg& s : segs)
+        if (s.n) std::memcpy(s.dst, s.src, s.n);
+      return;
+    }
+    Job job;
+    for (const Seg& s : segs)
+      for (size_t o = 0; o < s.n; o += kPiece)
+        job.pieces.push_back({static_cast<uint8_t*>(s.dst) + o,
+                              static_cast<const uint8_t*>(s.src) + o, std::min(kPiece, s.n - o)});
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      queue_.push_back(&job);
+    }
+    cv_.notify_all();
+    work(job);
+    std::unique_lock<std::mutex> lk(mu_);
+    unlink(&job);
+    done_.wait(lk, [&] { return job.users == 0; });
+  }
+
+ private:
+  static constexpr size_t kPiece = 1u << 20;
+  static constexpr size_t kInline = 256u << 10;
+  struct Job {
+    std::vector<Seg> pieces;
+    std::atomic<size_t> next{0};
+    int users = 0;  // workers inside work(); guarded by mu_
+  };
+
+  static void work(Job& j) {
+    for (size_t i; (i = j.next.fetch_add(1)) < j.pieces.size();)
+      std::memcpy(j.pieces[i].dst, j.pieces[i].src, j.pieces[i].n);
+  }
+
+  void unlink(Job* j) {
+    for (auto it = queue_.begin(); it != queue_.end(); ++it)
+      if (*it == j) {
+        queue_.erase(it);
+        return;
+      }
+  }
+
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+      if (stop_) return;
+      Job* j = queue_.front();
+      ++j->users;
+      lk.unlock();
+      work(*j);
+      lk.lock();
+      unlink(j);  // every piece is taken
+      if (--j->users == 0) done_.notify_all();
+    }
+  }
+
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::deque<Job*> queue_;
+  std::vector<std::thread> workers_;
+  bool stop_ = false;
+};
+
 // ---- device buffers ------------------------------------------------------------------
 
 struct DevBuf {
@@ -162,12 +260,29 @@ struct HostBuf {
   }
 };
 
-struct Lane {
+// One pipeline stage of the host-memory path: a stream, a pinned chunk buffer and its
+// device mirror ([n][cpitch]), and the pointer/coefficient tables for launches on it.
+struct Slot {
   hipStream_t stream = nullptr;
-  DevBuf shards;    // pitched shard workspace (host-memory entry points)
-  HostBuf stage;    // pinned mirror of `shards`
-  DevBuf meta;      // pointer tables + coefficient tables + status word
-  HostBuf hmeta;    // pinned staging for `meta`
+  hipEvent_t done = nullptr;
+  DevBuf dev;
+  HostBuf host;
+  DevBuf meta;
+  HostBuf hmeta;
+  std::shared_ptr<const Tables> meta_tables;  // what `meta` currently holds
+  size_t meta_pitch = 0;
+  void* meta_base = nullptr;
+  bool pending = false;  // a chunk's outputs wait in `host`
+  size_t off = 0, width = 0;
+};
+
+constexpr int kSlots = 3;
+// Column chunk: about this many bytes over all n shards per pipeline step.
+constexpr size_t kChunkBytes = 16u << 20;
+
+struct Lane {
+  Slot slot[kSlots];
+  HostBuf hstatus;  // pinned status words read back at the end of a call
 };
 
 struct Device {
@@ -261,17 +376,22 @@ struct rs_ctx {
   std::vector<std::unique_ptr<Device>> devs;
   std::atomic<unsigned> rr{0};
   TableCache cache;
+  CopyPool pool;
 
   ~rs_ctx() {
     for (auto& d : devs) {
       (void)hipSetDevice(d->id);
       for (auto& l : d->lanes) {
-        if (l->stream) (void)hipStreamSynchronize(l->stream);
-        l->shards.release();
-        l->stage.release();
-        l->meta.release();
-        l->hmeta.release();
-        if (l->stream) (void)hipStreamDestroy(l->stream);
+        for (Slot& sl : l->slot) {
+          if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+          sl.dev.release();
+          sl.host.release();
+          sl.meta.release();
+          sl.hmeta.release();
+          if (sl.done) (void)hipEventDestroy(sl.done);
+          if (sl.stream) (void)hipStreamDestroy(sl.stream);
+        }
+        l->hstatus.release();
       }
     }
   }
@@ -292,9 +412,12 @@ struct rs_ctx {
       }
       if (static_cast<int>(d->lanes.size()) < kMaxLanesPerDevice) {
         auto l = std::make_unique<Lane>();
-        if (hipSetDevice(d->id) != hipSuccess ||
-            hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess)
-          return nullptr;
+        if (hipSetDevice(d->id) != hipSuccess) return nullptr;
+        for (Slot& sl : l->slot)
+          if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess ||
+              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
+            return nullptr;
+        if (l->hstatus.ensure(kSlots * sizeof(int))) return nullptr;
         d->lanes.push_back(std::move(l));
         return d->lanes.back().get();
       }
@@ -322,49 +445,128 @@ struct LaneGuard {
   }
 };
 
-// Host-memory path: stage the k valid shards into the lane's pitched workspace, run
-// every group, copy the written shards back. in(i)/out(i) give host buffers by shard
-// index. Returns RS_OK / RS_E_CORRUPT (verify rows mismatched) / error.
+// Host-memory path (Codec.Encode/Decode ends, codec.go:21-78): the shard columns
+// [0, S) are cut into chunks that rotate through the lane's kSlots slots. Per chunk:
+// copy-pool copies of the input shards' columns into pinned memory, H2D, the kernel
+// groups, D2H of the written shards on the slot's stream; the CPU copies chunk j in
+// while the GPU/DMA work on chunks j-1 and j-2, and copies chunk j-kSlots out.
+// in(i)/out(i) give host buffers by shard index. Returns RS_OK, RS_E_CORRUPT (verify
+// rows mismatched) or an error.
 template <class InF, class OutF>
-int run_host(rs_ctx* ctx, const Tables& t, size_t S, InF host_in, OutF host_out) {
+int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, InF host_in,
+             OutF host_out) {
   if (ctx->devs.empty()) return RS_E_HIP;
+  const Tables& t = *tp;
   Device* dev = ctx->devs[ctx->rr.fetch_add(1) % ctx->devs.size()].get();
   LaneGuard lg{ctx, dev, ctx->acquire(dev)};
   if (!lg.lane) return RS_E_HIP;
   Lane& L = *lg.lane;
   HIPCHK(hipSetDevice(dev->id));
   const int n = t.k + t.m;
-  const size_t pitch = round_up(std::max<size_t>(S, 1), kPitchAlign);
-  int rc = L.shards.ensure(pitch * n);
-  if (rc) return rc;
-  if ((rc = L.stage.ensure(pitch * n))) return rc;
-  auto* dsh = static_cast<uint8_t*>(L.shards.p);
-  auto* hsh = static_cast<uint8_t*>(L.stage.p);
 
-  const MetaLayout ML = meta_layout(t, 1);
-  if ((rc = L.meta.ensure(ML.total))) return rc;
-  if ((rc = L.hmeta.ensure(ML.total))) return rc;
-  auto* dmeta = static_cast<uint8_t*>(L.meta.p);
-  const bool aligned = fill_meta(t, ML, 1, static_cast<uint8_t*>(L.hmeta.p),
-                                 [&](int, int i) { return dsh + pitch * i; });
-  HIPCHK(hipMemcpyAsync(dmeta, L.hmeta.p, ML.total, hipMemcpyHostToDevice, L.stream));
-
-  // inputs: valid shards + verify shards
   std::vector<int> ins(t.valid);
   ins.insert(ins.end(), t.check.begin(), t.check.end());
-  for (int i : ins) {
-    std::memcpy(hsh + pitch * i, host_in(i), S);
-    HIPCHK(hipMemcpyAsync(dsh + pitch * i, hsh + pitch * i, S, hipMemcpyHostToDevice, L.stream));
+  const std::vector<int>& outs = t.missing;
+  const int in_lo = *std::min_element(ins.begin(), ins.end());
+  const int in_hi = *std::max_element(ins.begin(), ins.end());
+  const int out_lo = outs.empty() ? 0 : *std::min_element(outs.begin(), outs.end());
+  const int out_hi = outs.empty() ? -1 : *std::max_element(outs.begin(), outs.end());
+
+  size_t cw = S;  // chunk width (bytes per shard), a multiple of 4 KiB unless one chunk
+  if (S * n > kChunkBytes) cw = std::max<size_t>(4096, kChunkBytes / n / 4096 * 4096);
+  const size_t cpitch = round_up(cw, kPitchAlign);
+  const size_t nchunks = (S + cw - 1) / cw;
+  const int nslots = static_cast<int>(std::min<size_t>(nchunks, kSlots));
+  const MetaLayout ML = meta_layout(t, 1);
+  // small chunks move as one contiguous row range instead of one copy per shard
+  const bool coalesce = cpitch * n <= (4u << 20);
+
+  for (int si = 0; si < nslots; ++si) {
+    Slot& sl = L.slot[si];
+    int rc;
+    if ((rc = sl.dev.ensure(cpitch * n)) || (rc = sl.host.ensure(cpitch * n)) ||
+        (rc = sl.meta.ensure(ML.total)) || (rc = sl.hmeta.ensure(ML.total)))
+      return rc;
+    if (sl.meta_tables != tp || sl.meta_pitch != cpitch || sl.meta_base != sl.dev.p) {
+      auto* base = static_cast<uint8_t*>(sl.dev.p);
+      fill_meta(t, ML, 1, static_cast<uint8_t*>(sl.hmeta.p),
+                [&](int, int i) { return base + cpitch * i; });
+      HIPCHK(hipMemcpyAsync(sl.meta.p, sl.hmeta.p, ML.total, hipMemcpyHostToDevice, sl.stream));
+      sl.meta_tables = tp;
+      sl.meta_pitch = cpitch;
+      sl.meta_base = sl.dev.p;
+    } else {
+      HIPCHK(hipMemsetAsync(static_cast<uint8_t*>(sl.meta.p) + ML.status_off, 0, sizeof(int),
+                            sl.stream));
+    }
+    sl.pending = false;
   }
-  HIPCHK(launch_groups(t, ML, 1, dmeta, S, aligned, L.stream));
-  for (int i : t.missing)
-    HIPCHK(hipMemcpyAsync(hsh + pitch * i, dsh + pitch * i, S, hipMemcpyDeviceToHost, L.stream));
+
+  std::vector<CopyPool::Seg> segs;
+  auto drain = [&](Slot& sl) -> int {
+    if (!sl.pending) return RS_OK;
+    HIPCHK(hipEventSynchronize(sl.done));
+    segs.clear();
+    auto* h = static_cast<uint8_t*>(sl.host.p);
+    for (int i : outs) segs.push_back({host_out(i) + sl.off, h + cpitch * i, sl.width});
+    ctx->pool.run(segs);
+    sl.pending = false;
+    return RS_OK;
+  };
+
+  for (size_t j = 0; j < nchunks; ++j) {
+    Slot& sl = L.slot[j % kSlots];
+    int rc = drain(sl);
+    if (rc) return rc;
+    const size_t off = j * cw, w = std::min(cw, S - off);
+    auto* h = static_cast<uint8_t*>(sl.host.p);
+    auto* d = static_cast<uint8_t*>(sl.dev.p);
+    segs.clear();
+    for (int i : ins) segs.push_back({h + cpitch * i, host_in(i) + off, w});
+    ctx->pool.run(segs);
+    if (coalesce) {
+      const size_t bytes = cpitch * (in_hi - in_lo) + w;
+      HIPCHK(hipMemcpyAsync(d + cpitch * in_lo, h + cpitch * in_lo, bytes,
+                            hipMemcpyHostToDevice, sl.stream));
+    } else {
+      for (int i : ins)
+        HIPCHK(hipMemcpyAsync(d + cpitch * i, h + cpitch * i, w, hipMemcpyHostToDevice,
+                              sl.stream));
+    }
+    HIPCHK(launch_groups(t, ML, 1, static_cast<uint8_t*>(sl.meta.p), w, true, sl.stream));
+    if (!outs.empty()) {
+      if (coalesce) {
+        const size_t bytes = cpitch * (out_hi - out_lo) + w;
+        HIPCHK(hipMemcpyAsync(h + cpitch * out_lo, d + cpitch * out_lo, bytes,
+                              hipMemcpyDeviceToHost, sl.stream));
+      } else {
+        for (int i : outs)
+          HIPCHK(hipMemcpyAsync(h + cpitch * i, d + cpitch * i, w, hipMemcpyDeviceToHost,
+                                sl.stream));
+      }
+    }
+    HIPCHK(hipEventRecord(sl.done, sl.stream));
+    sl.pending = true;
+    sl.off = off;
+    sl.width = w;
+  }
+  for (size_t j = nchunks > static_cast<size_t>(kSlots) ? nchunks - kSlots : 0; j < nchunks; ++j) {
+    int rc = drain(L.slot[j % kSlots]);
+    if (rc) return rc;
+  }
   int status = 0;
-  if (!t.check.empty())
-    HIPCHK(hipMemcpyAsync(&status, dmeta + ML.status_off, sizeof(int), hipMemcpyDeviceToHost,
-                          L.stream));
-  HIPCHK(hipStreamSynchronize(L.stream));
-  for (int i : t.missing) std::memcpy(host_out(i), hsh + pitch * i, S);
+  if (!t.check.empty()) {
+    auto* hs = static_cast<int*>(L.hstatus.p);
+    for (int si = 0; si < nslots; ++si) {
+      Slot& sl = L.slot[si];
+      HIPCHK(hipMemcpyAsync(hs + si, static_cast<uint8_t*>(sl.meta.p) + ML.status_off,
+                            sizeof(int), hipMemcpyDeviceToHost, sl.stream));
+    }
+    for (int si = 0; si < nslots; ++si) {
+      HIPCHK(hipStreamSynchronize(L.slot[si].stream));
+      status |= hs[si];
+    }
+  }
   return status ? RS_E_CORRUPT : RS_OK;
 }
 
@@ -404,7 +606,7 @@ int reconstruct_host(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* 
   auto t = ctx->cache.get(k, m, present, verify);
   if (!t) return RS_E_SINGULAR;
   if (t->groups.empty()) return RS_OK;
-  rc = run_host(ctx, *t, S, [&](int i) { return shards[i]; }, [&](int i) { return shards[i]; });
+  rc = run_host(ctx, t, S, [&](int i) { return shards[i]; }, [&](int i) { return shards[i]; });
   if (rc == RS_OK || rc == RS_E_CORRUPT)
     for (int i : t->missing) lens[i] = S;
   return rc;
@@ -504,7 +706,7 @@ int rs_encode(rs_ctx* ctx, int k, int m, size_t S, const uint8_t* const* data,
   for (int i = 0; i < k + m; ++i) present[i] = i < k;
   auto t = ctx->cache.get(k, m, present, false);
   if (!t) return RS_E_SINGULAR;
-  return run_host(ctx, *t, S, [&](int i) { return data[i]; },
+  return run_host(ctx, t, S, [&](int i) { return data[i]; },
                   [&](int i) { return parity[i - k]; });
 }
 
@@ -518,14 +720,22 @@ int rs_codec_encode(rs_ctx* ctx, int k, int m, const uint8_t* data, size_t len,
   const size_t S = (len + k - 1) / k;
   const int n = k + m;
   if (out_cap < S * n) return RS_E_ARG;
-  if (shards_out != data) std::memmove(shards_out, data, len);
+  if (shards_out != data) {
+    const bool overlap = shards_out < data + len && data < shards_out + S * n;
+    if (overlap) {
+      std::memmove(shards_out, data, len);
+    } else {
+      std::vector<CopyPool::Seg> segs{{shards_out, data, len}};
+      ctx->pool.run(segs);
+    }
+  }
   std::memset(shards_out + len, 0, S * k - len);  // Split zero padding
   *shard_size = S;
   uint8_t present[256];
   for (int i = 0; i < n; ++i) present[i] = i < k;
   auto t = ctx->cache.get(k, m, present, false);
   if (!t) return RS_E_SINGULAR;
-  return run_host(ctx, *t, S, [&](int i) { return shards_out + S * i; },
+  return run_host(ctx, t, S, [&](int i) { return shards_out + S * i; },
                   [&](int i) { return shards_out + S * i; });
 }
 
@@ -549,7 +759,7 @@ int rs_verify(rs_ctx* ctx, int k, int m, const uint8_t* const* shards, const siz
   for (int i = 0; i < n; ++i) present[i] = 1;
   auto t = ctx->cache.get(k, m, present, true);
   if (!t) return RS_E_SINGULAR;
-  rc = run_host(ctx, *t, S, [&](int i) { return shards[i]; },
+  rc = run_host(ctx, t, S, [&](int i) { return shards[i]; },
                 [&](int) { return static_cast<uint8_t*>(nullptr); });
   if (rc == RS_OK || rc == RS_E_CORRUPT) {
     *ok = rc == RS_OK;
@@ -570,11 +780,13 @@ int rs_codec_decode(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* l
   if (static_cast<uint64_t>(S) * k < static_cast<uint64_t>(original_size))
     return RS_E_INSUFFICIENT;
   size_t left = static_cast<size_t>(original_size);
+  std::vector<CopyPool::Seg> segs;
   for (int i = 0; i < k && left; ++i) {
     const size_t c = std::min(S, left);
-    std::memcpy(out + S * i, shards[i], c);
+    segs.push_back({out + S * i, shards[i], c});
     left -= c;
   }
+  ctx->pool.run(segs);
   return RS_OK;
 }
 

@@ -169,9 +169,10 @@ class Codec:
         mv = memoryview(out)
         return [mv[i * S:(i + 1) * S] for i in range(k + m)]
 
-    def decode(self, shards: List, profile: ErasureProfile, original_size: int) -> bytes:
+    def decode(self, shards: List, profile: ErasureProfile, original_size: int) -> bytearray:
         """codec.go:45-78. `None` or empty entries are missing shards; they are
-        reconstructed in place (the list is mutated, as Go mutates its [][]byte)."""
+        reconstructed in place (the list is mutated, as Go mutates its [][]byte).
+        Returns a fresh buffer of original_size bytes (Go: buf[:originalSize])."""
         k, m = profile.data_shards, profile.parity_shards
         if k < 1 or m < 1:
             raise ErrInvalidProfile()
@@ -198,7 +199,7 @@ class Codec:
                 if shards[i] is None or len(shards[i]) == 0:
                     shards[i] = bufs[i]
         if rc == N.RS_OK:
-            return bytes(out)
+            return out
         if rc == N.RS_E_CORRUPT:
             raise ErrShardCorrupted()
         if rc == N.RS_E_INSUFFICIENT:
