@@ -5,6 +5,7 @@ next to this file so it travels to the GPU box with the repo snapshot.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -24,11 +25,21 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def _digest() -> str:
+    h = hashlib.sha256(ARCH.encode())
+    for f in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
+    """Content-hash check (mtimes are not reliable across repo snapshots)."""
+    try:
+        with open(LIB + ".sha256") as fh:
+            return not os.path.exists(LIB) or fh.read().strip() != _digest()
+    except OSError:
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
 
 
 def build(force: bool = False, extra_flags=None) -> str:
@@ -51,6 +62,8 @@ def build(force: bool = False, extra_flags=None) -> str:
     os.replace(tmp, LIB)
     for o in objs:
         os.remove(o)
+    with open(LIB + ".sha256", "w") as fh:
+        fh.write(_digest())
     return LIB
 
 

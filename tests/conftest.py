@@ -8,6 +8,13 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def pytest_sessionstart(session):
+    """Build libcallfs_rs.so (no-op when its content hash is current) before any test
+    module imports callfs_amd, and the C oracle."""
+    import __graft_entry__
+    __graft_entry__.build()
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running")
@@ -15,8 +22,6 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def native_lib():
-    """Build (if stale) and load libcallfs_rs.so."""
-    from callfs_amd import build as b
-    b.build()
+    """libcallfs_rs.so, built at session start."""
     from callfs_amd import _native
     return _native
