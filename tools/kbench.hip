@@ -88,8 +88,8 @@ int main(int argc, char** argv) {
   const int B = argc > 4 ? std::atoi(argv[4]) : 256;
   const int rounds = argc > 5 ? std::atoi(argv[5]) : 5;
   const int iters = argc > 6 ? std::atoi(argv[6]) : 10;
-  if (k != 10 || m != 4) {
-    std::fprintf(stderr, "variants are instantiated for k=10 m=4\n");
+  if (m < 1 || m > 8 || k < 1 || k > 256) {
+    std::fprintf(stderr, "need 1<=m<=8, 1<=k<=256\n");
     return 2;
   }
   const int n = k + m;
@@ -138,21 +138,32 @@ int main(int argc, char** argv) {
   a.batch = B;
 
   using namespace dev;
+  using Prod = Policy<4, 1, true, true, false>;
   std::vector<Variant> vs;
-  vs.push_back(make_variant<10, 4, Policy<4, 1, false, false, false>>("prod wpe4 u1"));
-  vs.push_back(make_variant<10, 4, Policy<4, 1, true, true, false>>("nt wpe4 u1"));
-  vs.push_back(make_variant<10, 4, Policy<8, 1, true, true, false>>("nt wpe8 u1"));
-  vs.push_back(make_variant<10, 4, Policy<4, 2, true, true, false>>("nt wpe4 u2"));
-  vs.push_back(make_variant<0, 4, Policy<4, 1, false, false, false>>("rtK wpe4"));
-  vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, false>>("rtK nt wpe4"));
-  vs.push_back(make_variant<0, 4, Policy<8, 1, true, true, false>>("rtK nt wpe8"));
-  vs.push_back(make_variant<0, 4, Policy<4, 2, true, true, false>>("rtK nt u2"));
-  vs.push_back(make_variant<0, 4, Policy<2, 2, true, true, false>>("rtK nt u2 wpe2"));
-  vs.push_back(Variant{"xor-stream (ceiling)", [](const ApplyArgs& a, hipStream_t s) {
+  switch (m) {  // production kernel (runtime K) for this row count
+    case 1: vs.push_back(make_variant<0, 1, Prod>("prod rtK nt")); break;
+    case 2: vs.push_back(make_variant<0, 2, Prod>("prod rtK nt")); break;
+    case 3: vs.push_back(make_variant<0, 3, Prod>("prod rtK nt")); break;
+    case 4: vs.push_back(make_variant<0, 4, Prod>("prod rtK nt")); break;
+    case 5: vs.push_back(make_variant<0, 5, Prod>("prod rtK nt")); break;
+    case 6: vs.push_back(make_variant<0, 6, Prod>("prod rtK nt")); break;
+    case 7: vs.push_back(make_variant<0, 7, Prod>("prod rtK nt")); break;
+    case 8: vs.push_back(make_variant<0, 8, Prod>("prod rtK nt")); break;
+  }
+  const bool rs10_4 = k == 10 && m == 4;
+  if (rs10_4) {
+    vs.push_back(make_variant<10, 4, Policy<4, 1, false, false, false>>("ctK plain"));
+    vs.push_back(make_variant<10, 4, Policy<4, 1, true, true, false>>("ctK nt"));
+    vs.push_back(make_variant<0, 4, Policy<4, 1, false, false, false>>("rtK plain"));
+    vs.push_back(make_variant<0, 4, Policy<8, 1, true, true, false>>("rtK nt wpe8"));
+    vs.push_back(make_variant<0, 4, Policy<4, 2, true, true, false>>("rtK nt u2"));
+    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, true>>("rtK nt persist8", 8));
+  }
+  if (rs10_4) vs.push_back(Variant{"xor-stream (ceiling)", [](const ApplyArgs& a, hipStream_t s) {
                          const unsigned g = static_cast<unsigned>((a.nvec + 255) / 256 * a.batch);
                          hipLaunchKernelGGL((xor_stream<10, 4, false>), dim3(g), dim3(256), 0, s, a);
                        }, false});
-  vs.push_back(Variant{"xor-stream nt (ceiling)", [](const ApplyArgs& a, hipStream_t s) {
+  if (rs10_4) vs.push_back(Variant{"xor-stream nt (ceiling)", [](const ApplyArgs& a, hipStream_t s) {
                          const unsigned g = static_cast<unsigned>((a.nvec + 255) / 256 * a.batch);
                          hipLaunchKernelGGL((xor_stream<10, 4, true>), dim3(g), dim3(256), 0, s, a);
                        }, false});
