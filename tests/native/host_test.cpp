@@ -1,0 +1,139 @@
+// Host-side C++ of the RS path under sanitizers (built by tests/test_native_host.py
+// with g++ -fsanitize=address,undefined and -fsanitize=thread; no GPU needed).
+//  1. GF(2^8) field + matrices (gf256.hpp) against upstream known-answer values
+//  2. v_perm_b32 table packing: emulate the instruction on the CPU and check c*x for
+//     every (c, x), i.e. what rs_apply.hpp's gf_mul4 computes
+//  3. decode_plan rows reproduce erased shards for every 1..m erasure pattern subset
+//  4. CopyPool under concurrent callers
+#include <cstdio>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "copy_pool.hpp"
+#include "gf256.hpp"
+
+using namespace callfs;
+
+static int fails = 0;
+#define CHECK(c)                                                  \
+  do {                                                            \
+    if (!(c)) {                                                   \
+      std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c);     \
+      ++fails;                                                    \
+    }                                                             \
+  } while (0)
+
+// ISA semantics of v_perm_b32 D = perm(S0, S1, sel), bytes of {S0,S1} (S1 low).
+static uint32_t v_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  const uint64_t v = (static_cast<uint64_t>(s0) << 32) | s1;
+  uint32_t d = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t s = (sel >> (8 * i)) & 0xff;
+    uint32_t b;
+    if (s >= 13) b = 0xff;
+    else if (s == 12) b = 0;
+    else if (s >= 8) b = 0;  // sign-extension selects: never produced by the kernel
+    else b = (v >> (8 * s)) & 0xff;
+    d |= b << (8 * i);
+  }
+  return d;
+}
+
+int main() {
+  const GF& g = gf();
+  CHECK(g.mul[3][4] == 12 && g.mul[7][7] == 21 && g.mul[23][45] == 41);
+  CHECK(g.pow(2, 2) == 4 && g.pow(5, 20) == 235 && g.pow(13, 7) == 43 && g.pow(0, 0) == 1);
+  Mat E;
+  CHECK(encode_matrix(10, 4, E));
+  const uint8_t row0[10] = {129, 150, 175, 184, 210, 196, 254, 232, 3, 2};
+  for (int i = 0; i < 10; ++i) CHECK(E.at(10, i) == row0[i]);
+  CHECK(encode_matrix(5, 5, E));
+  {  // TestOneEncode RS(5,5)
+    const uint8_t d[5][2] = {{0, 1}, {4, 5}, {2, 3}, {6, 7}, {8, 9}};
+    const uint8_t want[5][2] = {{12, 13}, {10, 11}, {14, 15}, {90, 91}, {94, 95}};
+    for (int j = 0; j < 5; ++j)
+      for (int b = 0; b < 2; ++b) {
+        uint8_t v = 0;
+        for (int i = 0; i < 5; ++i) v ^= g.mul[E.at(5 + j, i)][d[i][b]];
+        CHECK(v == want[j][b]);
+      }
+  }
+  // 2. v_perm tables: every coefficient, every byte value, 4 lanes of a dword
+  for (int c = 0; c < 256; ++c) {
+    uint32_t t[kTabWords];
+    perm_tables(static_cast<uint8_t>(c), t);
+    for (int x0 = 0; x0 < 256; x0 += 1) {
+      const uint32_t x = static_cast<uint32_t>(x0) | (static_cast<uint32_t>(255 - x0) << 8) |
+                         (static_cast<uint32_t>((x0 * 7) & 255) << 16) |
+                         (static_cast<uint32_t>((x0 ^ 0x5a)) << 24);
+      const uint32_t i0 = x & 0x07070707u, i1 = (x >> 3) & 0x07070707u, i2 = (x >> 6) & 0x03030303u;
+      const uint32_t p = v_perm(t[1], t[0], i0) ^ v_perm(t[3], t[2], i1) ^ v_perm(t[4], t[4], i2);
+      for (int b = 0; b < 4; ++b)
+        CHECK(((p >> (8 * b)) & 0xff) == g.mul[c][(x >> (8 * b)) & 0xff]);
+    }
+  }
+  // 3. decode rows: every erasure pattern of RS(6,3) up to 3 erasures
+  {
+    const int k = 6, m = 3, n = 9, S = 64;
+    std::mt19937 rng(1);
+    Mat E2;
+    encode_matrix(k, m, E2);
+    std::vector<std::vector<uint8_t>> sh(n, std::vector<uint8_t>(S));
+    for (int i = 0; i < k; ++i)
+      for (auto& b : sh[i]) b = rng() & 0xff;
+    for (int j = 0; j < m; ++j)
+      for (int b = 0; b < S; ++b) {
+        uint8_t v = 0;
+        for (int i = 0; i < k; ++i) v ^= g.mul[E2.at(k + j, i)][sh[i][b]];
+        sh[k + j][b] = v;
+      }
+    int patterns = 0;
+    for (int mask = 0; mask < (1 << n); ++mask) {
+      if (__builtin_popcount(mask) > m) continue;
+      uint8_t present[16];
+      for (int i = 0; i < n; ++i) present[i] = !((mask >> i) & 1);
+      DecodePlan dp;
+      CHECK(decode_plan(k, m, present, dp));
+      for (size_t r = 0; r < dp.missing.size() + dp.check.size(); ++r) {
+        const int idx = r < dp.missing.size() ? dp.missing[r] : dp.check[r - dp.missing.size()];
+        for (int b = 0; b < S; ++b) {
+          uint8_t v = 0;
+          for (int i = 0; i < k; ++i) v ^= g.mul[dp.rows.at(static_cast<int>(r), i)][sh[dp.valid[i]][b]];
+          CHECK(v == sh[idx][b]);
+        }
+      }
+      ++patterns;
+    }
+    CHECK(patterns == 1 + 9 + 36 + 84);
+  }
+  // 4. copy pool: 6 concurrent callers, ragged segments
+  {
+    CopyPool pool;
+    std::vector<std::thread> ts;
+    std::atomic<int> bad{0};
+    for (int t = 0; t < 6; ++t)
+      ts.emplace_back([&, t] {
+        std::mt19937 rng(100 + t);
+        for (int it = 0; it < 20; ++it) {
+          const size_t nseg = 1 + rng() % 7;
+          std::vector<std::vector<uint8_t>> src(nseg), dst(nseg);
+          std::vector<CopyPool::Seg> segs;
+          for (size_t s = 0; s < nseg; ++s) {
+            const size_t len = rng() % (3u << 20);
+            src[s].resize(len);
+            for (size_t b = 0; b < len; b += 4093) src[s][b] = static_cast<uint8_t>(rng());
+            dst[s].assign(len, 0xEE);
+            segs.push_back({dst[s].data(), src[s].data(), len});
+          }
+          pool.run(segs);
+          for (size_t s = 0; s < nseg; ++s)
+            if (src[s] != dst[s]) bad++;
+        }
+      });
+    for (auto& th : ts) th.join();
+    CHECK(bad == 0);
+  }
+  std::printf(fails ? "FAILED %d\n" : "host_test ok\n", fails);
+  return fails ? 1 : 0;
+}

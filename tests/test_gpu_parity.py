@@ -310,12 +310,13 @@ def test_plan_misaligned_pointers(native_lib):
 
 
 def test_full_size_config_rs10_4_64mib_roundtrip(native_lib):
-    """configs[1]/[2] at full object size (64 MiB, S = 6,710,887): encode a batch,
-    erase 4 shards per pattern, decode, and require the bytes back bit-exact; sample
-    stripes checked against the oracle (size-independent properties)."""
+    """configs[1]/[2] at full size: 256 objects of 64 MiB (S = 6,710,887; 22.4 GiB of
+    shards in HBM). Encode the batch, erase 4 shards per pattern, decode, require every
+    byte back (size-independent round-trip property); stripe 0 checked against the
+    oracle."""
     import torch
     from callfs_amd.device import Plan
-    k, m, S, batch = 10, 4, 6_710_887, 32
+    k, m, S, batch = 10, 4, 6_710_887, 256
     sb = _batch(k, m, S, batch, seed=64)
     enc = Plan.for_batch(sb)
     enc.launch()
