@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "libcallfs_rs.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
-        f"{LIB_PATH} is missing: build it with `python -m callfs_amd.build` "
+        f"{LIB_PATH} is missing: build it with `python callfs_amd/build.py` "
         "(hipcc --offload-arch=gfx950); the RS path has no CPU fallback")
 
 # PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7, loaded by file
@@ -75,6 +75,12 @@ SIGNATURES = {
     "rs_plan_destroy": (None, [_vp]),
     "rs_encode_dev": (_int, [_vp, _int, _int, _int, _sz, _int, ctypes.POINTER(_vp), _vp]),
     "rs_decode_dev": (_int, [_vp, _int, _int, _int, _sz, _int, _u8p, ctypes.POINTER(_vp), _vp]),
+    "rs_sha256_plan_create": (_int, [_vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64),
+                                     _int, ctypes.POINTER(_vp)]),
+    "rs_sha256_plan_launch": (_int, [_vp, _vp, _vp]),
+    "rs_sha256_plan_destroy": (None, [_vp]),
+    "rs_sha256_dev": (_int, [_vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64), _int,
+                             _vp, _vp]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

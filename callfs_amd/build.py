@@ -1,6 +1,6 @@
 """Build libcallfs_rs.so (HIP kernels + C ABI) in-tree for gfx950.
 
-`python -m callfs_amd.build` or `__graft_entry__.build()`. The shared library lands
+`python callfs_amd/build.py` or `__graft_entry__.build()`. The shared library lands
 next to this file so it travels to the GPU box with the repo snapshot.
 """
 from __future__ import annotations
@@ -13,8 +13,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcallfs_rs.so")
-SOURCES = ["rs_kernels.hip", "rs_capi.cpp"]
-HEADERS = ["rs_kernels.hpp", "rs_apply.hpp", "gf256.hpp", "copy_pool.hpp", os.path.join("..", "..", "include", "callfs_rs.h")]
+SOURCES = ["rs_kernels.hip", "sha256.hip", "rs_capi.cpp"]
+HEADERS = ["rs_kernels.hpp", "rs_apply.hpp", "gf256.hpp", "copy_pool.hpp", "sha256.hpp", os.path.join("..", "..", "include", "callfs_rs.h")]
 ARCH = os.environ.get("CALLFS_OFFLOAD_ARCH", "gfx950")
 
 

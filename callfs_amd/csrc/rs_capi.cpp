@@ -31,6 +31,7 @@
 #include "copy_pool.hpp"
 #include "gf256.hpp"
 #include "rs_kernels.hpp"
+#include "sha256.hpp"
 
 using namespace callfs;
 
@@ -800,6 +801,73 @@ int rs_decode_dev(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
                   const uint8_t* present, uint8_t* const* shards, void* stream) {
   if (!present) return RS_E_ARG;
   return one_shot(ctx, device, k, m, S, batch, present, shards, stream);
+}
+
+// ---- batched SHA-256 (ShardChecksum) ------------------------------------------------
+
+struct rs_hash_plan {
+  int device = 0;
+  int count = 0;
+  int mpw = 1;
+  void* dtab = nullptr;  // [count] pointers then [count] lengths
+};
+
+int rs_sha256_plan_create(rs_ctx* ctx, int device, const uint8_t* const* msgs,
+                          const uint64_t* lens, int count, rs_hash_plan** out) {
+  if (!ctx || !out || count < 0 || (count && (!msgs || !lens))) return RS_E_ARG;
+  *out = nullptr;
+  if (!ctx->device(device)) return RS_E_ARG;
+  auto plan = std::make_unique<rs_hash_plan>();
+  plan->device = device;
+  plan->count = count;
+  plan->mpw = default_msgs_per_wave(count);
+  if (const char* e = std::getenv("CALLFS_SHA_MSGS_PER_WAVE")) plan->mpw = std::atoi(e);
+  HIPCHK(hipSetDevice(device));
+  const size_t bytes = static_cast<size_t>(count) * (sizeof(void*) + sizeof(uint64_t));
+  if (count) {
+    std::vector<uint8_t> h(bytes);
+    std::memcpy(h.data(), msgs, count * sizeof(void*));
+    std::memcpy(h.data() + count * sizeof(void*), lens, count * sizeof(uint64_t));
+    if (hipMalloc(&plan->dtab, bytes) != hipSuccess) return RS_E_NOMEM;
+    if (hipMemcpy(plan->dtab, h.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(plan->dtab);
+      return RS_E_HIP;
+    }
+  }
+  *out = plan.release();
+  return RS_OK;
+}
+
+int rs_sha256_plan_launch(rs_hash_plan* plan, uint8_t* digests, void* stream) {
+  if (!plan || (plan->count && !digests)) return RS_E_ARG;
+  if ((reinterpret_cast<uintptr_t>(digests) & 3u) != 0) return RS_E_ARG;
+  HIPCHK(hipSetDevice(plan->device));
+  Sha256Args a{};
+  a.msgs = static_cast<const uint8_t* const*>(plan->dtab);
+  a.lens = reinterpret_cast<const uint64_t*>(static_cast<uint8_t*>(plan->dtab) +
+                                             plan->count * sizeof(void*));
+  a.digests = reinterpret_cast<uint32_t*>(digests);
+  a.count = plan->count;
+  HIPCHK(launch_sha256(a, plan->mpw, static_cast<hipStream_t>(stream)));
+  return RS_OK;
+}
+
+void rs_sha256_plan_destroy(rs_hash_plan* plan) {
+  if (!plan) return;
+  (void)hipSetDevice(plan->device);
+  if (plan->dtab) (void)hipFree(plan->dtab);
+  delete plan;
+}
+
+int rs_sha256_dev(rs_ctx* ctx, int device, const uint8_t* const* msgs, const uint64_t* lens,
+                  int count, uint8_t* digests, void* stream) {
+  rs_hash_plan* p = nullptr;
+  int rc = rs_sha256_plan_create(ctx, device, msgs, lens, count, &p);
+  if (rc) return rc;
+  rc = rs_sha256_plan_launch(p, digests, stream);
+  if (!rc && hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) rc = RS_E_HIP;
+  rs_sha256_plan_destroy(p);
+  return rc;
 }
 
 }  // extern "C"

@@ -113,3 +113,57 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+class HashPlan:
+    """Batched SHA-256 (erasure.ShardChecksum, codec.go:81-84) of device-resident
+    messages: rs_sha256_plan_* over `pointers`/`lengths` (device addresses, bytes)."""
+
+    def __init__(self, pointers: Sequence[int], lengths: Sequence[int], device: int = 0,
+                 context: Optional[N.Context] = None):
+        self.ctx = context or N.default_context()
+        if len(pointers) != len(lengths):
+            raise ValueError("pointers/lengths length mismatch")
+        self.count = len(pointers)
+        self.device = device
+        ptrs = (ctypes.c_void_p * max(1, self.count))(*pointers)
+        lens = (ctypes.c_uint64 * max(1, self.count))(*lengths)
+        h = ctypes.c_void_p()
+        N.check(N.lib.rs_sha256_plan_create(self.ctx.handle, device, ptrs, lens, self.count,
+                                            ctypes.byref(h)), "rs_sha256_plan_create")
+        self.handle = h
+
+    def launch(self, digests: torch.Tensor, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """digests: uint8 CUDA tensor of at least 32*count bytes (4-B aligned)."""
+        if digests.dtype != torch.uint8 or digests.numel() < 32 * self.count:
+            raise ValueError("need a uint8 tensor of 32*count bytes")
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        N.check(N.lib.rs_sha256_plan_launch(self.handle, ctypes.c_void_p(digests.data_ptr()),
+                                            ctypes.c_void_p(s.cuda_stream)), "rs_sha256_plan_launch")
+
+    def hexdigests(self) -> list:
+        out = torch.empty(32 * max(1, self.count), dtype=torch.uint8,
+                          device=torch.device("cuda", self.device))
+        self.launch(out)
+        raw = out.cpu().numpy().tobytes()
+        return [raw[32 * i:32 * (i + 1)].hex() for i in range(self.count)]
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            N.lib.rs_sha256_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def shard_checksums(sb: StripeBatch) -> list:
+    """ShardChecksum of every shard of a device-resident batch: [stripe][shard] hex."""
+    dev = sb.device.index if sb.device.index is not None else 0
+    hp = HashPlan(sb.pointers(), [sb.S] * (sb.batch * sb.n), dev)
+    flat = hp.hexdigests()
+    hp.close()
+    return [flat[b * sb.n:(b + 1) * sb.n] for b in range(sb.batch)]

@@ -126,6 +126,22 @@ int rs_encode_dev(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
 int rs_decode_dev(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
                   const uint8_t* present, uint8_t* const* shards, void* stream);
 
+/* ---- ShardChecksum on device-resident shards (codec.go:81-84; §8(f) of SURVEY.md) ----
+ * SHA-256 of `count` messages already in HBM, one digest per message written to
+ * `digests` (device memory, 32*count bytes, FIPS 180-4 byte order — hex-encode it for
+ * the Go string). msgs/lens are HOST arrays of device pointers and byte lengths.
+ * SHA-256 is serial within a message, so this pays off only in batches of many shards
+ * (scrub, device-resident pipelines); a single request's checksums stay on the CPU.
+ * rs_sha256_plan_* upload the message table once; rs_sha256_dev is the one-shot form
+ * (synchronous on `stream`). */
+typedef struct rs_hash_plan rs_hash_plan;
+int  rs_sha256_plan_create(rs_ctx* ctx, int device, const uint8_t* const* msgs,
+                           const uint64_t* lens, int count, rs_hash_plan** out);
+int  rs_sha256_plan_launch(rs_hash_plan* plan, uint8_t* digests, void* stream);
+void rs_sha256_plan_destroy(rs_hash_plan* plan);
+int  rs_sha256_dev(rs_ctx* ctx, int device, const uint8_t* const* msgs, const uint64_t* lens,
+                   int count, uint8_t* digests, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
