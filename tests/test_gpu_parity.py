@@ -332,3 +332,26 @@ def test_full_size_config_rs10_4_64mib_roundtrip(native_lib):
         dec.launch()
         assert not dec.corrupt()
         assert torch.equal(sb.buf[:, :, :S], ref[:, :, :S]), erase
+
+
+@pytest.mark.parametrize("k,m", [(200, 56), (255, 1), (128, 128), (1, 255)])
+def test_max_profiles_roundtrip(codec, k, m):
+    """k+m = 256 is the largest GF(2^8) profile (upstream switches to Leopard above)."""
+    from callfs_amd import ErasureProfile
+    L = 256 * 1024 + 13
+    data = rnd(k * 1000 + m, L)
+    got = codec.encode(data, ErasureProfile(k, m))
+    want = oracle_shards(data, k, m)
+    assert all(bytes(g) == w.tobytes() for g, w in zip(got, want))
+    rng = np.random.default_rng(k + m)
+    erase = set(rng.choice(k + m, size=min(m, 9), replace=False).tolist())
+    shards = [None if i in erase else bytes(s) for i, s in enumerate(got)]
+    assert codec.decode(shards, ErasureProfile(k, m), L) == data
+
+
+def test_leopard_profiles_unsupported(codec):
+    from callfs_amd import ErasureProfile, ErrUnsupportedProfile
+    with pytest.raises(ErrUnsupportedProfile):
+        codec.encode(b"x" * 1000, ErasureProfile(200, 57))
+    with pytest.raises(ErrUnsupportedProfile):
+        codec.decode([b"x"] * 257, ErasureProfile(200, 57), 10)
