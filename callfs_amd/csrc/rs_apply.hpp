@@ -78,13 +78,19 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //   U        16-B column vectors per lane (tile = 256*U vectors of a stripe)
 //   NT_LOAD  / NT_STORE: non-temporal (streaming) global loads / stores
 //   PERSIST  grid-stride over tiles with a fixed grid instead of one tile per block
-template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_>
+//   BS       threads per block; PD prefetch depth in input-shard pairs (1 or 2)
+//   ORD      tile order: 0 = a stripe's tiles consecutive, 1 = interleaved across stripes
+template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
+          int PD_ = 1, int ORD_ = 0>
 struct Policy {
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
   static constexpr bool NT_LOAD = NT_LOAD_;
   static constexpr bool NT_STORE = NT_STORE_;
   static constexpr bool PERSIST = PERSIST_;
+  static constexpr int BS = BS_;
+  static constexpr int PD = PD_;
+  static constexpr int ORD = ORD_;
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -137,35 +143,43 @@ __device__ __forceinline__ void mac_one(uint32_t (&acc)[U][RT][4], const uint4 (
     }
 }
 
-// Tiles: a stripe's nvec vectors are cut into tiles of 256*U; tile t covers stripe
-// t / tiles_per_stripe. Every tile is wave-uniform in its stripe, so shard pointers
-// stay scalar.
+// Tiles: a stripe's nvec vectors are cut into tiles of BS*U; tile t covers stripe
+// t / tiles_per_stripe (ORD 0) or t % batch (ORD 1). Every tile is wave-uniform in its
+// stripe, so shard pointers stay scalar.
 template <int KT, int RT, class P>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P::WPE, 8)))
+__global__ __launch_bounds__(P::BS) __attribute__((amdgpu_waves_per_eu(P::WPE, 8)))
 void rs_apply_vec(ApplyArgs a) {
   constexpr int U = P::U;
+  constexpr int BS = P::BS;
   const int K = KT ? KT : a.K;
   const int npairs = K >> 1;
-  const uint32_t tile_vecs = kBlock * U;
+  const uint32_t tile_vecs = BS * U;
   const uint32_t tps = static_cast<uint32_t>((a.nvec + tile_vecs - 1) / tile_vecs);
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
   const cptr<uint32_t> tabs = as_const(a.tabs);
 
   for (uint32_t t = blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
-    const uint32_t stripe = t / tps;
-    const uint64_t v0 = static_cast<uint64_t>(t - stripe * tps) * tile_vecs + threadIdx.x;
+    uint32_t stripe, tile;
+    if constexpr (P::ORD == 0) {
+      stripe = t / tps;
+      tile = t - stripe * tps;
+    } else {
+      tile = t / static_cast<uint32_t>(a.batch);
+      stripe = t - tile * static_cast<uint32_t>(a.batch);
+    }
+    const uint64_t v0 = static_cast<uint64_t>(tile) * tile_vecs + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * RT;
     bool live[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) live[u] = v0 + static_cast<uint64_t>(u) * kBlock < a.nvec;
+    for (int u = 0; u < U; ++u) live[u] = v0 + static_cast<uint64_t>(u) * BS < a.nvec;
     if (!live[0]) continue;
 
     auto ld = [&](int i, uint4 (&x)[U]) {
       const uint4* src = reinterpret_cast<const uint4*>(in[i]) + v0;
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        x[u] = (u == 0 || live[u]) ? load16<P>(src + u * kBlock) : make_uint4(0, 0, 0, 0);
+        x[u] = (u == 0 || live[u]) ? load16<P>(src + u * BS) : make_uint4(0, 0, 0, 0);
     };
 
     uint32_t acc[U][RT][4];
@@ -176,24 +190,37 @@ void rs_apply_vec(ApplyArgs a) {
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[u][r][w] = 0;
 
-    uint4 xa[U], xb[U];
+    // register ring of PD+1 input pairs: pair p is consumed while pairs p+1..p+PD load
+    uint4 xa[U], xb[U], ya[U], yb[U];
     if (npairs) {
       ld(0, xa);
       ld(1, xb);
     }
+    if (P::PD > 1 && npairs > 1) {
+      ld(2, ya);
+      ld(3, yb);
+    }
 #pragma unroll 1
     for (int p = 0; p < npairs; ++p) {
-      uint4 ya[U], yb[U];
-      if (p + 1 < npairs) {
-        ld(2 * p + 2, ya);
-        ld(2 * p + 3, yb);
+      uint4 za[U], zb[U];
+      const int nxt = p + P::PD;
+      if (nxt < npairs) {
+        ld(2 * nxt, za);
+        ld(2 * nxt + 1, zb);
       }
       const cptr<uint32_t> ta = tabs + static_cast<size_t>(2 * p) * RT * 5;
       mac_pair<RT, U>(acc, xa, xb, ta, ta + RT * 5);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        xa[u] = ya[u];
-        xb[u] = yb[u];
+        if constexpr (P::PD > 1) {
+          xa[u] = ya[u];
+          xb[u] = yb[u];
+          ya[u] = za[u];
+          yb[u] = zb[u];
+        } else {
+          xa[u] = za[u];
+          xb[u] = zb[u];
+        }
       }
     }
     if (K & 1) {
@@ -211,10 +238,10 @@ void rs_apply_vec(ApplyArgs a) {
         if (!live[u]) continue;
         const uint4 o = make_uint4(acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]);
         if (cmp) {
-          const uint4 y = dst[u * kBlock];
+          const uint4 y = dst[u * BS];
           bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) != 0;
         } else {
-          store16<P>(dst + u * kBlock, o);
+          store16<P>(dst + u * BS, o);
         }
       }
     }
@@ -255,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_bytes(ApplyArgs a, uint64_t b
 // `blocks_per_cu` blocks on each of the 256 CUs.
 template <class P>
 inline unsigned vec_grid(uint64_t nvec, int batch, int blocks_per_cu = 8) {
-  const uint64_t tile = static_cast<uint64_t>(kBlock) * P::U;
+  const uint64_t tile = static_cast<uint64_t>(P::BS) * P::U;
   const uint64_t ntiles = (nvec + tile - 1) / tile * static_cast<uint64_t>(batch);
   if (P::PERSIST) return static_cast<unsigned>(std::min<uint64_t>(ntiles, 256ull * blocks_per_cu));
   return static_cast<unsigned>(ntiles);

@@ -13,11 +13,12 @@ namespace {
 
 using dev::kBlock;
 
-// Production policy (tools/kbench.hip, MI355X, RS(10,4) 1 MiB shards x 256 stripes):
-// runtime-K pair loop + non-temporal loads and stores = 6027 GB/s (75.3% of 8 TB/s),
-// vs 5457 GB/s for compile-time K with plain loads/stores and 5927 GB/s for an
-// XOR-only kernel with every load hoisted (DESIGN.md "Kernel tuning log").
-using ProdPolicy = dev::Policy<4, 1, true, true, false>;
+// Production policy (tools/kbench.hip on MI355X, RS(10,4) 1 MiB shards x 256 stripes,
+// DESIGN.md "Kernel tuning log"): runtime-K pair loop, non-temporal loads and stores,
+// 512-thread blocks, two input pairs in flight = 6118-6168 GB/s (76.5-77.1 % of
+// 8 TB/s) vs 5457 GB/s for the first compile-time-K / plain-load version and
+// 5957 GB/s for an XOR-only kernel with the same loads and stores.
+using ProdPolicy = dev::Policy<4, 1, true, true, false, 512, 2, 0>;
 
 using VecFn = void (*)(ApplyArgs);
 using ByteFn = void (*)(ApplyArgs, uint64_t);
@@ -48,7 +49,7 @@ hipError_t launch_apply(ApplyArgs a, bool aligned, hipStream_t stream) {
     if (a.nvec) {
       const unsigned gx = dev::vec_grid<ProdPolicy>(a.nvec, a.batch);
       VecFn fn = kVec[a.R - 1];
-      hipLaunchKernelGGL(fn, dim3(gx), dim3(kBlock), 0, stream, a);
+      hipLaunchKernelGGL(fn, dim3(gx), dim3(ProdPolicy::BS), 0, stream, a);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }

@@ -77,7 +77,7 @@ template <int K, int R, class P>
 Variant make_variant(const char* name, int blocks_per_cu = 8) {
   return Variant{name, [blocks_per_cu](const ApplyArgs& a, hipStream_t s) {
                    const unsigned g = dev::vec_grid<P>(a.nvec, a.batch, blocks_per_cu);
-                   hipLaunchKernelGGL((dev::rs_apply_vec<K, R, P>), dim3(g), dim3(256), 0, s, a);
+                   hipLaunchKernelGGL((dev::rs_apply_vec<K, R, P>), dim3(g), dim3(P::BS), 0, s, a);
                  }};
 }
 
@@ -138,7 +138,7 @@ int main(int argc, char** argv) {
   a.batch = B;
 
   using namespace dev;
-  using Prod = Policy<4, 1, true, true, false>;
+  using Prod = Policy<4, 1, true, true, false, 512, 2, 0>;  // = rs_kernels.hip ProdPolicy
   std::vector<Variant> vs;
   switch (m) {  // production kernel (runtime K) for this row count
     case 1: vs.push_back(make_variant<0, 1, Prod>("prod rtK nt")); break;
@@ -152,12 +152,15 @@ int main(int argc, char** argv) {
   }
   const bool rs10_4 = k == 10 && m == 4;
   if (rs10_4) {
-    vs.push_back(make_variant<10, 4, Policy<4, 1, false, false, false>>("ctK plain"));
-    vs.push_back(make_variant<10, 4, Policy<4, 1, true, true, false>>("ctK nt"));
-    vs.push_back(make_variant<0, 4, Policy<4, 1, false, false, false>>("rtK plain"));
-    vs.push_back(make_variant<0, 4, Policy<8, 1, true, true, false>>("rtK nt wpe8"));
-    vs.push_back(make_variant<0, 4, Policy<4, 2, true, true, false>>("rtK nt u2"));
-    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, true>>("rtK nt persist8", 8));
+    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, false, 512, 2, 0>>("bs512 pd2"));
+    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, false, 512, 1, 0>>("bs512 pd1"));
+    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, false, 1024, 2, 0>>("bs1024 pd2"));
+    vs.push_back(make_variant<0, 4, Policy<2, 1, true, true, false, 512, 2, 0>>("bs512 pd2 wpe2"));
+    vs.push_back(make_variant<0, 4, Policy<6, 1, true, true, false, 512, 2, 0>>("bs512 pd2 wpe6"));
+    vs.push_back(make_variant<0, 4, Policy<8, 1, true, true, false, 512, 2, 0>>("bs512 pd2 wpe8"));
+    vs.push_back(make_variant<0, 4, Policy<4, 2, true, true, false, 512, 2, 0>>("bs512 pd2 u2"));
+    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, true, 512, 2, 0>>("bs512 pd2 persist", 4));
+    vs.push_back(make_variant<10, 4, Policy<4, 1, true, true, false, 512, 2, 0>>("ctK bs512 pd2"));
   }
   if (rs10_4) vs.push_back(Variant{"xor-stream (ceiling)", [](const ApplyArgs& a, hipStream_t s) {
                          const unsigned g = static_cast<unsigned>((a.nvec + 255) / 256 * a.batch);
