@@ -21,6 +21,9 @@
 //  * Ragged tails (S % 16) and unaligned shard pointers take the byte kernel.
 #pragma once
 
+#include <algorithm>
+#include <type_traits>
+
 #include "rs_kernels.hpp"
 
 namespace callfs {
@@ -79,7 +82,8 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //   NT_LOAD  / NT_STORE: non-temporal (streaming) global loads / stores
 //   PERSIST  grid-stride over tiles with a fixed grid instead of one tile per block
 //   BS       threads per block; PD prefetch depth in input-shard pairs (1 or 2)
-//   ORD      tile order: 0 = a stripe's tiles consecutive, 1 = interleaved across stripes
+//   ORD      tile order: 0 = a stripe's tiles consecutive, 1 = interleaved across all
+//            stripes, 2/3 = interleaved within groups of 8/32 stripes
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
           int PD_ = 1, int ORD_ = 0>
 struct Policy {
@@ -163,9 +167,17 @@ void rs_apply_vec(ApplyArgs a) {
     if constexpr (P::ORD == 0) {
       stripe = t / tps;
       tile = t - stripe * tps;
-    } else {
+    } else if constexpr (P::ORD == 1) {
       tile = t / static_cast<uint32_t>(a.batch);
       stripe = t - tile * static_cast<uint32_t>(a.batch);
+    } else {
+      // groups of G stripes, tiles interleaved across the group's stripes
+      constexpr uint32_t G = P::ORD == 2 ? 8 : 32;
+      const uint32_t per_group = G * tps;
+      const uint32_t g = t / per_group, r = t - g * per_group;
+      const uint32_t gsz = std::min<uint32_t>(G, static_cast<uint32_t>(a.batch) - g * G);
+      tile = r / gsz;
+      stripe = g * G + (r - tile * gsz);
     }
     const uint64_t v0 = static_cast<uint64_t>(tile) * tile_vecs + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
@@ -243,6 +255,121 @@ void rs_apply_vec(ApplyArgs a) {
         } else {
           store16<P>(dst + u * BS, o);
         }
+      }
+    }
+    if (bad) atomicOr(a.status, 1);
+  }
+}
+
+// ---- LDS nibble-table variant ---------------------------------------------------------
+// Per data byte two ds_read_b64 lookups (low / high nibble) return the products for all
+// RT <= 8 rows at once, so the cost per data dword is about 20 VALU + 8 LDS reads for
+// any RT, versus 5 + 4.5*RT VALU for the v_perm kernel. Tables: 256 B per input shard
+// at LDS offset 256*i (low table at +0, high at +128), loaded once per block.
+// Addresses: xl = (x << 3) & 0x78787878 holds 8*low-nibble per byte, xh the same for the
+// high nibble with bit 7 set (the +128); v_perm(base_i, xl, {j,5,6,7}) drops byte j into
+// byte 0 of the 256-B-aligned table base: one VALU per lookup.
+// Accumulation is per data-byte position (T[w][j] = 8 row products of byte j of dword w,
+// XORed over the shards); a final byte transpose (3 VALU per row) forms the row words.
+template <int RT>
+struct LdsAcc {
+  static constexpr bool WIDE = RT > 4;
+  using T = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
+};
+
+template <int RT>
+__device__ __forceinline__ typename LdsAcc<RT>::T lds_lookup(const uint8_t* smem, uint32_t addr) {
+  return *reinterpret_cast<const typename LdsAcc<RT>::T*>(smem + addr);
+}
+
+template <int RT>
+__device__ __forceinline__ void lds_mac(typename LdsAcc<RT>::T (&acc)[4][4], const uint4& x,
+                                        const uint8_t* smem, uint32_t base) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t xw = word(x, w);
+    const uint32_t xl = (xw << 3) & 0x78787878u;
+    const uint32_t xh = ((xw >> 1) & 0x78787878u) | 0x80808080u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t sel = 0x07060500u | static_cast<uint32_t>(j);
+      const auto lo = lds_lookup<RT>(smem, __builtin_amdgcn_perm(base, xl, sel));
+      const auto hi = lds_lookup<RT>(smem, __builtin_amdgcn_perm(base, xh, sel));
+      acc[w][j] ^= lo ^ hi;
+    }
+  }
+}
+
+// Row r's word = byte r of T[0..3].
+template <int RT>
+__device__ __forceinline__ uint32_t lds_row(const typename LdsAcc<RT>::T (&t)[4], int r) {
+  uint32_t t0, t1, t2, t3;
+  int rr = r;
+  if constexpr (LdsAcc<RT>::WIDE) {
+    const int sh = r >= 4 ? 32 : 0;
+    t0 = static_cast<uint32_t>(t[0] >> sh);
+    t1 = static_cast<uint32_t>(t[1] >> sh);
+    t2 = static_cast<uint32_t>(t[2] >> sh);
+    t3 = static_cast<uint32_t>(t[3] >> sh);
+    rr = r & 3;
+  } else {
+    t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3];
+  }
+  const uint32_t lo = __builtin_amdgcn_perm(t1, t0, 0x0c0c0400u | (0x0101u * rr));
+  const uint32_t hi = __builtin_amdgcn_perm(t3, t2, 0x04000c0cu | (0x01010000u * rr));
+  return lo | hi;
+}
+
+template <int RT, class P>
+__global__ __launch_bounds__(P::BS) __attribute__((amdgpu_waves_per_eu(P::WPE, 8)))
+void rs_apply_lds(ApplyArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int BS = P::BS;
+  using AccT = typename LdsAcc<RT>::T;
+  const int K = a.K;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.ltabs);
+    uint4* dst = reinterpret_cast<uint4*>(smem);
+    for (int j = threadIdx.x; j < K * 16; j += BS) dst[j] = src[j];
+  }
+  __syncthreads();
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + BS - 1) / BS);
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
+  for (uint32_t t = blockIdx.x; t < ntiles; t += ntiles) {
+    const uint32_t stripe = t / tps;
+    const uint64_t v0 = static_cast<uint64_t>(t - stripe * tps) * BS + threadIdx.x;
+    if (v0 >= a.nvec) continue;
+    cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
+    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * RT;
+    auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
+
+    AccT acc[4][4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[w][j] = 0;
+
+    // ring of three shard vectors: shard i is consumed while i+1, i+2 load
+    uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = x0;
+#pragma unroll 1
+    for (int i = 0; i < K; ++i) {
+      if (i + 2 < K) x2 = ld(i + 2);
+      lds_mac<RT>(acc, x0, smem, static_cast<uint32_t>(i) * 256u);
+      x0 = x1;
+      x1 = x2;
+    }
+
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const uint4 o = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
+                                 lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
+      uint4* dst = reinterpret_cast<uint4*>(out[r]) + v0;
+      if ((a.verify_mask >> r) & 1u) {
+        const uint4 y = *dst;
+        bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) != 0;
+      } else {
+        store16<P>(dst, o);
       }
     }
     if (bad) atomicOr(a.status, 1);

@@ -59,7 +59,8 @@ int check_profile(int k, int m) {
 struct Group {
   std::vector<int> shard;     // shard index per row
   uint32_t verify_mask = 0;   // bit r: compare row r (Verify) instead of storing it
-  std::vector<uint32_t> tabs; // [k][R][5]
+  std::vector<uint32_t> tabs; // [k][R][5] v_perm tables
+  std::vector<uint64_t> ltabs;  // [k][32] LDS nibble tables (used for R >= 5)
 };
 
 struct Tables {
@@ -92,6 +93,12 @@ std::shared_ptr<const Tables> build_tables(int k, int m, const uint8_t* present,
       if (is_check) g.verify_mask |= 1u << r;
       for (int i = 0; i < k; ++i)
         perm_tables(dp.rows.at(row, i), &g.tabs[(static_cast<size_t>(i) * R + r) * kTabWords]);
+    }
+    g.ltabs.assign(static_cast<size_t>(k) * 32, 0);
+    for (int i = 0; i < k; ++i) {
+      uint8_t col[8] = {0};
+      for (int r = 0; r < R; ++r) col[r] = dp.rows.at(g0 + r, i);
+      nibble_tables(col, R, &g.ltabs[static_cast<size_t>(i) * 32]);
     }
     t->groups.push_back(std::move(g));
   }
@@ -202,7 +209,7 @@ struct Device {
 // Device-side layout of everything one set of launches needs, packed into one buffer.
 struct MetaLayout {
   size_t in_off = 0, status_off = 0, total = 0;
-  std::vector<size_t> out_off, tab_off;
+  std::vector<size_t> out_off, tab_off, ltab_off;
 };
 
 MetaLayout meta_layout(const Tables& t, int batch) {
@@ -218,6 +225,7 @@ MetaLayout meta_layout(const Tables& t, int batch) {
   for (const Group& g : t.groups) {
     L.out_off.push_back(take(sizeof(void*) * static_cast<size_t>(batch) * g.shard.size()));
     L.tab_off.push_back(take(sizeof(uint32_t) * g.tabs.size()));
+    L.ltab_off.push_back(take(sizeof(uint64_t) * g.ltabs.size()));
   }
   L.total = off;
   return L;
@@ -245,6 +253,7 @@ bool fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F sh
         note(out[b * R + r]);
       }
     std::memcpy(h + L.tab_off[gi], g.tabs.data(), g.tabs.size() * sizeof(uint32_t));
+    std::memcpy(h + L.ltab_off[gi], g.ltabs.data(), g.ltabs.size() * sizeof(uint64_t));
   }
   return aligned;
 }
@@ -257,6 +266,7 @@ hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_
     a.in_tab = reinterpret_cast<const uint8_t* const*>(d + L.in_off);
     a.out_tab = reinterpret_cast<uint8_t* const*>(d + L.out_off[gi]);
     a.tabs = reinterpret_cast<const uint32_t*>(d + L.tab_off[gi]);
+    a.ltabs = reinterpret_cast<const uint64_t*>(d + L.ltab_off[gi]);
     a.S = S;
     a.verify_mask = g.verify_mask;
     a.status = reinterpret_cast<int*>(d + L.status_off);
@@ -359,15 +369,32 @@ struct LaneGuard {
 // in(i)/out(i) give host buffers by shard index. Returns RS_OK, RS_E_CORRUPT (verify
 // rows mismatched) or an error.
 template <class InF, class OutF>
+int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const Tables>& tp,
+                  size_t S, InF host_in, OutF host_out);
+
+template <class InF, class OutF>
 int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, InF host_in,
              OutF host_out) {
   if (ctx->devs.empty()) return RS_E_HIP;
-  const Tables& t = *tp;
   Device* dev = ctx->devs[ctx->rr.fetch_add(1) % ctx->devs.size()].get();
   LaneGuard lg{ctx, dev, ctx->acquire(dev)};
   if (!lg.lane) return RS_E_HIP;
-  Lane& L = *lg.lane;
-  HIPCHK(hipSetDevice(dev->id));
+  const int rc = run_host_impl(ctx, *lg.lane, dev->id, tp, S, host_in, host_out);
+  if (rc != RS_OK && rc != RS_E_CORRUPT) {
+    // never hand a lane with work in flight to the next caller
+    for (Slot& sl : lg.lane->slot) {
+      if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+      sl.pending = false;
+    }
+  }
+  return rc;
+}
+
+template <class InF, class OutF>
+int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const Tables>& tp,
+                  size_t S, InF host_in, OutF host_out) {
+  const Tables& t = *tp;
+  HIPCHK(hipSetDevice(device));
   const int n = t.k + t.m;
 
   std::vector<int> ins(t.valid);

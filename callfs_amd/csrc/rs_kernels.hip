@@ -20,6 +20,12 @@ using dev::kBlock;
 // 5957 GB/s for an XOR-only kernel with the same loads and stores.
 using ProdPolicy = dev::Policy<4, 1, true, true, false, 512, 2, 0>;
 
+// Row groups of 5..8 use the LDS nibble-table kernel: its cost does not grow with the
+// row count (RS(10,8): 5,749 vs 4,887 GB/s; RS(32,8): 4,783 vs 3,948; RS(12,6): 5,318
+// vs 5,118 — tools/kbench.hip), while for R <= 4 the v_perm kernel is faster.
+using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
+constexpr int kLdsMinRows = 5;
+
 using VecFn = void (*)(ApplyArgs);
 using ByteFn = void (*)(ApplyArgs, uint64_t);
 
@@ -29,11 +35,17 @@ constexpr auto vec_table(std::integer_sequence<int, Rs...>) {
 }
 
 template <int... Rs>
+constexpr auto lds_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsPolicy>...};
+}
+
+template <int... Rs>
 constexpr auto byte_table(std::integer_sequence<int, Rs...>) {
   return std::array<ByteFn, sizeof...(Rs)>{&dev::rs_apply_bytes<Rs + 1>...};
 }
 
 const auto kVec = vec_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
+const auto kLds = lds_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
 }  // namespace
@@ -47,9 +59,13 @@ hipError_t launch_apply(ApplyArgs a, bool aligned, hipStream_t stream) {
     a.nvec = a.S / 16;
     tail0 = a.nvec * 16;
     if (a.nvec) {
-      const unsigned gx = dev::vec_grid<ProdPolicy>(a.nvec, a.batch);
-      VecFn fn = kVec[a.R - 1];
-      hipLaunchKernelGGL(fn, dim3(gx), dim3(ProdPolicy::BS), 0, stream, a);
+      if (a.R >= kLdsMinRows && a.ltabs) {
+        const unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
+        hipLaunchKernelGGL(kLds[a.R - 1], dim3(gx), dim3(LdsPolicy::BS), a.K * 256, stream, a);
+      } else {
+        const unsigned gx = dev::vec_grid<ProdPolicy>(a.nvec, a.batch);
+        hipLaunchKernelGGL(kVec[a.R - 1], dim3(gx), dim3(ProdPolicy::BS), 0, stream, a);
+      }
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }

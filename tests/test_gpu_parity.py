@@ -125,8 +125,10 @@ def test_golden_fixtures(codec):
         assert got == case["shard_sha256"], case["name"]
 
 
+# R = m rows per launch group: 1..4 take the v_perm kernel, 5..8 the LDS nibble-table
+# kernel, m > 8 splits into several groups (9 = 8+1, 10 = 8+2, 20 = 8+8+4).
 PROFILES = [(1, 1), (2, 1), (3, 2), (4, 2), (5, 5), (6, 3), (8, 4), (10, 4), (12, 4),
-            (16, 4), (17, 3), (20, 10), (32, 8), (6, 9), (40, 20)]
+            (16, 4), (17, 3), (10, 6), (12, 7), (20, 10), (32, 8), (6, 9), (40, 20)]
 
 
 @pytest.mark.parametrize("k,m", PROFILES)

@@ -67,6 +67,12 @@ __global__ __launch_bounds__(256) void xor_stream(ApplyArgs a) {
     dev::store16<P>(reinterpret_cast<uint4*>(out[r]) + v, make_uint4(acc.x + r, acc.y, acc.z, acc.w));
 }
 
+template <int R, class P>
+void launch_lds(const ApplyArgs& a, hipStream_t s) {
+  const unsigned g = static_cast<unsigned>((a.nvec + P::BS - 1) / P::BS * a.batch);
+  hipLaunchKernelGGL((dev::rs_apply_lds<R, P>), dim3(g), dim3(P::BS), a.K * 256, s, a);
+}
+
 struct Variant {
   std::string name;
   std::function<void(const ApplyArgs&, hipStream_t)> launch;
@@ -88,12 +94,13 @@ int main(int argc, char** argv) {
   const int B = argc > 4 ? std::atoi(argv[4]) : 256;
   const int rounds = argc > 5 ? std::atoi(argv[5]) : 5;
   const int iters = argc > 6 ? std::atoi(argv[6]) : 10;
+  const size_t palign = argc > 7 ? std::strtoull(argv[7], nullptr, 0) : 256;
   if (m < 1 || m > 8 || k < 1 || k > 256) {
     std::fprintf(stderr, "need 1<=m<=8, 1<=k<=256\n");
     return 2;
   }
   const int n = k + m;
-  const size_t pitch = (S + 255) / 256 * 256;
+  const size_t pitch = (S + palign - 1) / palign * palign;
   const size_t total = pitch * n * B;
   uint8_t* buf;
   CK(hipMalloc(&buf, total));
@@ -108,17 +115,25 @@ int main(int argc, char** argv) {
   std::vector<uint32_t> tabs(static_cast<size_t>(k) * m * 5);
   for (int i = 0; i < k; ++i)
     for (int r = 0; r < m; ++r) perm_tables(E.at(k + r, i), &tabs[(static_cast<size_t>(i) * m + r) * 5]);
+  std::vector<uint64_t> ltabs(static_cast<size_t>(k) * 32);
+  for (int i = 0; i < k; ++i) {
+    uint8_t col[8] = {0};
+    for (int r = 0; r < m && r < 8; ++r) col[r] = E.at(k + r, i);
+    nibble_tables(col, m, &ltabs[static_cast<size_t>(i) * 32]);
+  }
   std::vector<const uint8_t*> in(static_cast<size_t>(B) * k);
   std::vector<uint8_t*> out(static_cast<size_t>(B) * m);
   for (int b = 0; b < B; ++b) {
     for (int i = 0; i < k; ++i) in[b * k + i] = buf + (static_cast<size_t>(b) * n + i) * pitch;
     for (int r = 0; r < m; ++r) out[b * m + r] = buf + (static_cast<size_t>(b) * n + k + r) * pitch;
   }
-  void *d_in, *d_out, *d_tabs;
+  void *d_in, *d_out, *d_tabs, *d_ltabs;
   int* d_status;
   CK(hipMalloc(&d_in, in.size() * sizeof(void*)));
   CK(hipMalloc(&d_out, out.size() * sizeof(void*)));
   CK(hipMalloc(&d_tabs, tabs.size() * 4));
+  CK(hipMalloc(&d_ltabs, ltabs.size() * 8));
+  CK(hipMemcpy(d_ltabs, ltabs.data(), ltabs.size() * 8, hipMemcpyHostToDevice));
   CK(hipMalloc(&d_status, 4));
   CK(hipMemcpy(d_in, in.data(), in.size() * sizeof(void*), hipMemcpyHostToDevice));
   CK(hipMemcpy(d_out, out.data(), out.size() * sizeof(void*), hipMemcpyHostToDevice));
@@ -129,6 +144,7 @@ int main(int argc, char** argv) {
   a.in_tab = static_cast<const uint8_t* const*>(d_in);
   a.out_tab = static_cast<uint8_t* const*>(d_out);
   a.tabs = static_cast<const uint32_t*>(d_tabs);
+  a.ltabs = static_cast<const uint64_t*>(d_ltabs);
   a.S = S;
   a.nvec = S / 16;
   a.verify_mask = 0;
@@ -151,16 +167,27 @@ int main(int argc, char** argv) {
     case 8: vs.push_back(make_variant<0, 8, Prod>("prod rtK nt")); break;
   }
   const bool rs10_4 = k == 10 && m == 4;
-  if (rs10_4) {
-    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, false, 512, 2, 0>>("bs512 pd2"));
-    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, false, 512, 1, 0>>("bs512 pd1"));
-    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, false, 1024, 2, 0>>("bs1024 pd2"));
-    vs.push_back(make_variant<0, 4, Policy<2, 1, true, true, false, 512, 2, 0>>("bs512 pd2 wpe2"));
-    vs.push_back(make_variant<0, 4, Policy<6, 1, true, true, false, 512, 2, 0>>("bs512 pd2 wpe6"));
-    vs.push_back(make_variant<0, 4, Policy<8, 1, true, true, false, 512, 2, 0>>("bs512 pd2 wpe8"));
-    vs.push_back(make_variant<0, 4, Policy<4, 2, true, true, false, 512, 2, 0>>("bs512 pd2 u2"));
-    vs.push_back(make_variant<0, 4, Policy<4, 1, true, true, true, 512, 2, 0>>("bs512 pd2 persist", 4));
-    vs.push_back(make_variant<10, 4, Policy<4, 1, true, true, false, 512, 2, 0>>("ctK bs512 pd2"));
+  using L512 = Policy<4, 1, true, true, false, 512, 2, 0>;
+  using L256 = Policy<4, 1, true, true, false, 256, 2, 0>;
+  using L512w2 = Policy<2, 1, true, true, false, 512, 2, 0>;
+  switch (m) {
+    case 4:
+      vs.push_back(Variant{"lds bs512", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, L512>(a, s); }});
+      vs.push_back(Variant{"lds bs256", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, L256>(a, s); }});
+      vs.push_back(Variant{"lds bs512 wpe2", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, L512w2>(a, s); }});
+      break;
+    case 8:
+      vs.push_back(Variant{"lds bs512 (prod R>=5)", [](const ApplyArgs& a, hipStream_t s) { launch_lds<8, L512w2>(a, s); }});
+      vs.push_back(Variant{"lds bs512", [](const ApplyArgs& a, hipStream_t s) { launch_lds<8, L512>(a, s); }});
+      vs.push_back(Variant{"lds bs256", [](const ApplyArgs& a, hipStream_t s) { launch_lds<8, L256>(a, s); }});
+      vs.push_back(Variant{"lds bs512 wpe2", [](const ApplyArgs& a, hipStream_t s) { launch_lds<8, L512w2>(a, s); }});
+      break;
+    case 2:
+      vs.push_back(Variant{"lds bs512", [](const ApplyArgs& a, hipStream_t s) { launch_lds<2, L512>(a, s); }});
+      break;
+    case 6:
+      vs.push_back(Variant{"lds bs512", [](const ApplyArgs& a, hipStream_t s) { launch_lds<6, L512>(a, s); }});
+      break;
   }
   if (rs10_4) vs.push_back(Variant{"xor-stream (ceiling)", [](const ApplyArgs& a, hipStream_t s) {
                          const unsigned g = static_cast<unsigned>((a.nvec + 255) / 256 * a.batch);
@@ -217,8 +244,8 @@ int main(int argc, char** argv) {
       }
     }
   }
-  std::printf("RS(%d,%d) S=%zu stripes=%d  working set %.2f GiB  rounds=%d iters=%d\n", k, m, S, B,
-              total / 1073741824.0, rounds, iters);
+  std::printf("RS(%d,%d) S=%zu pitch=%zu stripes=%d  working set %.2f GiB  rounds=%d iters=%d\n", k, m,
+              S, pitch, B, total / 1073741824.0, rounds, iters);
   std::printf("%-28s %10s %10s %10s %8s\n", "variant", "med_us", "min_us", "GB/s(med)", "%8TB/s");
   for (size_t vi = 0; vi < vs.size(); ++vi) {
     auto v = ms[vi];
