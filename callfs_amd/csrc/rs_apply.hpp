@@ -257,7 +257,7 @@ void rs_apply_vec(ApplyArgs a) {
         }
       }
     }
-    if (bad) atomicOr(a.status, 1);
+    if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
   }
 }
 
@@ -372,7 +372,7 @@ void rs_apply_lds(ApplyArgs a) {
         store16<P>(dst, o);
       }
     }
-    if (bad) atomicOr(a.status, 1);
+    if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
   }
 }
 
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_bytes(ApplyArgs a, uint64_t b
       if ((a.verify_mask >> r) & 1u) bad |= out[r][b] != v;
       else out[r][b] = v;
     }
-    if (bad) atomicOr(a.status, 1);
+    if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
   }
 }
 

@@ -220,7 +220,7 @@ MetaLayout meta_layout(const Tables& t, int batch) {
     off = round_up(off + bytes, 256);
     return o;
   };
-  L.status_off = take(sizeof(int));
+  L.status_off = take(sizeof(int) * static_cast<size_t>(batch));
   L.in_off = take(sizeof(void*) * static_cast<size_t>(batch) * t.k);
   for (const Group& g : t.groups) {
     L.out_off.push_back(take(sizeof(void*) * static_cast<size_t>(batch) * g.shard.size()));
@@ -234,7 +234,7 @@ MetaLayout meta_layout(const Tables& t, int batch) {
 // Fill host staging for the meta buffer. shard_ptr(b, i) gives stripe b's shard i.
 template <class F>
 bool fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
-  std::memset(h + L.status_off, 0, sizeof(int));
+  std::memset(h + L.status_off, 0, sizeof(int) * static_cast<size_t>(batch));
   auto* in = reinterpret_cast<const uint8_t**>(h + L.in_off);
   bool aligned = true;
   auto note = [&](const void* p) { aligned &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
@@ -259,7 +259,7 @@ bool fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F sh
 }
 
 hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_t* d, size_t S,
-                         bool aligned, hipStream_t s) {
+                         bool aligned, hipStream_t s, int status_stride = 0) {
   for (size_t gi = 0; gi < t.groups.size(); ++gi) {
     const Group& g = t.groups[gi];
     ApplyArgs a{};
@@ -270,6 +270,7 @@ hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_
     a.S = S;
     a.verify_mask = g.verify_mask;
     a.status = reinterpret_cast<int*>(d + L.status_off);
+    a.status_stride = status_stride;
     a.K = t.k;
     a.R = static_cast<int>(g.shard.size());
     a.batch = batch;
@@ -309,6 +310,7 @@ struct rs_ctx {
         }
         l->hstatus.release();
       }
+
     }
   }
 

@@ -21,7 +21,8 @@ struct ApplyArgs {
   uint64_t S;                    // shard bytes
   uint64_t nvec;                 // 16-byte vectors per shard handled by the vector kernel
   uint32_t verify_mask;
-  int* status;
+  int* status;                   // mismatch flag; stripe b uses status[b * status_stride]
+  int status_stride;
   int K;
   int R;
   int batch;

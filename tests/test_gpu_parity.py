@@ -357,3 +357,42 @@ def test_leopard_profiles_unsupported(codec):
         codec.encode(b"x" * 1000, ErasureProfile(200, 57))
     with pytest.raises(ErrUnsupportedProfile):
         codec.decode([b"x"] * 257, ErasureProfile(200, 57), 10)
+
+
+def test_small_objects_concurrent(codec):
+    """Small requests of mixed sizes and erasure patterns from 12 threads sharing one
+    Codec (lanes of one device, reused slot tables): every result exact, and a
+    corrupted request fails alone."""
+    from callfs_amd import ErasureProfile, ErrShardCorrupted
+    profile = ErasureProfile(10, 4)
+    errors = []
+
+    def work(tid):
+        try:
+            rng = np.random.default_rng(500 + tid)
+            for j in range(40):
+                L = int(rng.integers(1, 60_000))
+                data = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+                got = [bytes(s) for s in codec.encode(data, profile)]
+                want = oracle_shards(data, 10, 4)
+                assert all(g == w.tobytes() for g, w in zip(got, want)), (tid, j, L)
+                erase = set(rng.choice(14, size=int(rng.integers(0, 5)), replace=False).tolist())
+                shards = [None if i in erase else got[i] for i in range(14)]
+                if tid == 3 and j % 5 == 0 and len(erase) < 4:
+                    extra = [i for i in range(14) if i not in erase][10:]
+                    bad = bytearray(shards[extra[0]])
+                    bad[0] ^= 0x55
+                    shards[extra[0]] = bytes(bad)
+                    with pytest.raises(ErrShardCorrupted):
+                        codec.decode(shards, profile, L)
+                else:
+                    assert codec.decode(shards, profile, L) == data, (tid, j, L, erase)
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=work, args=(t,)) for t in range(12)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:3]

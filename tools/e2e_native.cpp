@@ -1,0 +1,114 @@
+// End-to-end host-memory RS throughput through the C ABI from native threads — the way
+// the Go server's request goroutines would call it (one cgo call per request), without
+// Python in the loop. Development tool, not product.
+//
+// build: g++ -O2 -std=c++17 -I include tools/e2e_native.cpp -L callfs_amd -lcallfs_rs \
+//          -Wl,-rpath,'$ORIGIN/../callfs_amd' -lpthread -o tools/e2e_native
+// run:   tools/e2e_native k m object_bytes threads seconds [erase,list]
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "callfs_rs.h"
+
+int main(int argc, char** argv) {
+  if (argc < 6) {
+    std::fprintf(stderr, "usage: %s k m object_bytes threads seconds [erase,list]\n", argv[0]);
+    return 2;
+  }
+  const int k = std::atoi(argv[1]), m = std::atoi(argv[2]), n = k + m;
+  const size_t L = std::strtoull(argv[3], nullptr, 0);
+  const int T = std::atoi(argv[4]);
+  const double secs = std::atof(argv[5]);
+  std::vector<int> erase;
+  if (argc > 6) {
+    std::string e(argv[6]);
+    for (size_t p = 0; p < e.size();) {
+      size_t q = e.find(',', p);
+      if (q == std::string::npos) q = e.size();
+      if (q > p) erase.push_back(std::atoi(e.substr(p, q - p).c_str()));
+      p = q + 1;
+    }
+  }
+  rs_ctx* ctx = nullptr;
+  if (rs_init(&ctx, 0) != RS_OK) {
+    std::fprintf(stderr, "rs_init failed\n");
+    return 1;
+  }
+  const size_t S = (L + k - 1) / k;
+  struct Thr {
+    std::vector<uint8_t> src, enc, out;
+    std::vector<std::vector<uint8_t>> sh;
+    long ops = 0;
+    int err = 0;
+  };
+  std::vector<Thr> th(T);
+  for (int t = 0; t < T; ++t) {
+    std::mt19937_64 rng(1234 + t);
+    th[t].src.resize(L);
+    for (auto& b : th[t].src) b = static_cast<uint8_t>(rng());
+    th[t].enc.resize(n * S);
+    th[t].out.resize(L);
+    size_t ss = 0;
+    if (rs_codec_encode(ctx, k, m, th[t].src.data(), L, th[t].enc.data(), n * S, &ss) != RS_OK) return 1;
+    th[t].sh.assign(n, std::vector<uint8_t>(S));
+    for (int i = 0; i < n; ++i) std::memcpy(th[t].sh[i].data(), th[t].enc.data() + S * i, S);
+  }
+  auto run = [&](bool encode) {
+    std::atomic<bool> stop{false};
+    std::vector<std::thread> ws;
+    for (int t = 0; t < T; ++t) {
+      th[t].ops = 0;
+      ws.emplace_back([&, t] {
+        Thr& me = th[t];
+        std::vector<uint8_t> enc2(n * S);
+        std::vector<uint8_t*> ptrs(n);
+        std::vector<size_t> lens(n);
+        while (!stop.load(std::memory_order_relaxed)) {
+          int rc;
+          if (encode) {
+            size_t ss = 0;
+            rc = rs_codec_encode(ctx, k, m, me.src.data(), L, enc2.data(), n * S, &ss);
+          } else {
+            // present shards were fetched once before the loop; the erased ones are
+            // rebuilt into their buffers by every call
+            for (int i = 0; i < n; ++i) {
+              bool gone = false;
+              for (int e : erase) gone |= e == i;
+              ptrs[i] = me.sh[i].data();
+              lens[i] = gone ? 0 : S;
+            }
+            rc = rs_codec_decode(ctx, k, m, ptrs.data(), lens.data(), me.out.data(),
+                                 static_cast<int64_t>(L));
+          }
+          if (rc != RS_OK) me.err = rc;
+          ++me.ops;
+        }
+      });
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+    stop = true;
+    for (auto& w : ws) w.join();
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    long ops = 0;
+    for (auto& x : th) ops += x.ops;
+    return std::make_pair(ops / el * L / 1073741824.0, ops);
+  };
+  auto e = run(true);
+  auto d = run(false);
+  int bad = 0;
+  for (auto& x : th) bad |= x.err || x.out != x.src;
+  std::printf("{\"api\": \"native\", \"k\": %d, \"m\": %d, \"object_bytes\": %zu, \"threads\": %d, "
+              "\"erase_count\": %zu, \"encode_gib_s\": %.3f, \"decode_gib_s\": %.3f, "
+              "\"encode_calls\": %ld, \"decode_calls\": %ld, \"ok\": %s}\n",
+              k, m, L, T, erase.size(), e.first, d.first, e.second, d.second, bad ? "false" : "true");
+  rs_shutdown(ctx);
+  return bad ? 1 : 0;
+}
