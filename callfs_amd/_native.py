@@ -71,6 +71,7 @@ SIGNATURES = {
                               ctypes.POINTER(_vp)]),
     "rs_plan_launch": (_int, [_vp, _vp]),
     "rs_plan_status": (_int, [_vp, _vp, ctypes.POINTER(_int)]),
+    "rs_plan_stripe_status": (_int, [_vp, _vp, ctypes.POINTER(_int)]),
     "rs_plan_bytes": (ctypes.c_uint64, [_vp]),
     "rs_plan_destroy": (None, [_vp]),
     "rs_encode_dev": (_int, [_vp, _int, _int, _int, _sz, _int, ctypes.POINTER(_vp), _vp]),

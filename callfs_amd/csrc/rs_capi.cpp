@@ -782,20 +782,28 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
   HIPCHK(hipSetDevice(plan->device));
   HIPCHK(launch_groups(*plan->tables, plan->layout, plan->batch,
                        static_cast<uint8_t*>(plan->dmeta), plan->S, plan->aligned,
-                       static_cast<hipStream_t>(stream)));
+                       static_cast<hipStream_t>(stream), /*status_stride=*/1));
+  return RS_OK;
+}
+
+int rs_plan_stripe_status(rs_plan* plan, void* stream, int* flags) {
+  if (!plan || !flags) return RS_E_ARG;
+  HIPCHK(hipSetDevice(plan->device));
+  auto s = static_cast<hipStream_t>(stream);
+  auto* st = static_cast<uint8_t*>(plan->dmeta) + plan->layout.status_off;
+  const size_t bytes = sizeof(int) * static_cast<size_t>(plan->batch);
+  HIPCHK(hipMemcpyAsync(flags, st, bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemsetAsync(st, 0, bytes, s));
+  HIPCHK(hipStreamSynchronize(s));
   return RS_OK;
 }
 
 int rs_plan_status(rs_plan* plan, void* stream, int* corrupt) {
   if (!plan || !corrupt) return RS_E_ARG;
-  HIPCHK(hipSetDevice(plan->device));
-  auto s = static_cast<hipStream_t>(stream);
-  auto* st = static_cast<uint8_t*>(plan->dmeta) + plan->layout.status_off;
-  int v = 0;
-  HIPCHK(hipMemcpyAsync(&v, st, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemsetAsync(st, 0, sizeof(int), s));
-  HIPCHK(hipStreamSynchronize(s));
-  *corrupt = v != 0;
+  std::vector<int> flags(static_cast<size_t>(plan->batch));
+  const int rc = rs_plan_stripe_status(plan, stream, flags.data());
+  if (rc) return rc;
+  *corrupt = std::any_of(flags.begin(), flags.end(), [](int f) { return f != 0; });
   return RS_OK;
 }
 

@@ -103,6 +103,15 @@ class Plan:
                                      ctypes.byref(c)), "rs_plan_status")
         return bool(c.value)
 
+    def corrupt_stripes(self, stream: Optional[torch.cuda.Stream] = None) -> list:
+        """Synchronises the stream; indices of the stripes whose Verify rows mismatched
+        since the last status call (then clears)."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        flags = (ctypes.c_int * self.batch)()
+        N.check(N.lib.rs_plan_stripe_status(self.handle, ctypes.c_void_p(s.cuda_stream), flags),
+                "rs_plan_stripe_status")
+        return [b for b in range(self.batch) if flags[b]]
+
     def close(self) -> None:
         if getattr(self, "handle", None):
             N.lib.rs_plan_destroy(self.handle)

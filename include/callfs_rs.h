@@ -108,13 +108,17 @@ int rs_verify(rs_ctx* ctx, int k, int m, const uint8_t* const* shards, const siz
  * re-checks the remaining present parity (the Verify of codec.go:59), OR-ing 1 into
  * the plan's device status word on mismatch. rs_plan_launch only enqueues work on
  * `stream` (a hipStream_t; NULL = the null stream) — no allocation, no sync.
- * rs_plan_status synchronises `stream`, returns the status word in *corrupt and
- * clears it. rs_plan_bytes: algorithmic HBM bytes one launch moves
- * (reads of the k+verify inputs + writes of the missing shards). */
+ * rs_plan_status synchronises `stream`, sets *corrupt when any stripe's verify rows
+ * mismatched since the last status call, and clears the flags;
+ * rs_plan_stripe_status does the same per stripe (flags: `batch` ints, nonzero =
+ * that object is corrupt — ErrShardCorrupted for it alone). rs_plan_bytes: algorithmic
+ * HBM bytes one launch moves (reads of the k+verify inputs + writes of the missing
+ * shards). */
 int  rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
                     const uint8_t* present, uint8_t* const* shards, rs_plan** out);
 int  rs_plan_launch(rs_plan* plan, void* stream);
 int  rs_plan_status(rs_plan* plan, void* stream, int* corrupt);
+int  rs_plan_stripe_status(rs_plan* plan, void* stream, int* flags);
 uint64_t rs_plan_bytes(const rs_plan* plan);
 void rs_plan_destroy(rs_plan* plan);
 

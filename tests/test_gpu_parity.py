@@ -286,12 +286,18 @@ def test_plan_decode_restores_and_verifies(native_lib, erase):
     dec.launch()
     assert not dec.corrupt()
     assert torch.equal(sb.buf[:, :, :S], ref[:, :, :S])
-    # corrupt a parity shard outside the first k present: Verify must flag it
+    # corrupt a parity shard outside the first k present: Verify must flag exactly the
+    # stripes that were touched
     extra = [i for i in range(k + m) if present[i]][k:]
     if extra:
         sb.buf[3, extra[0], 1000] ^= 1
+        sb.buf[6, extra[-1], S - 1] ^= 0x80
+        dec.launch()
+        assert dec.corrupt_stripes() == [3, 6]
         dec.launch()
         assert dec.corrupt()
+        dec.launch()
+        assert dec.corrupt_stripes() == [3, 6]
 
 
 def test_plan_misaligned_pointers(native_lib):
