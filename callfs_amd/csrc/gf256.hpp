@@ -185,21 +185,22 @@ inline void perm_tables(uint8_t c, uint32_t out[kTabWords]) {
   out[4] = pack(t2);      // T2
 }
 
-// LDS nibble tables for one input shard over up to 8 output rows: entry e (0..15) of
-// the low table holds c_r * e in byte r, entry e of the high table c_r * (e << 4);
-// out[0..15] = low, out[16..31] = high. 256 B per shard; a 16 x 8-B table spans 32
-// distinct LDS banks, so random lookups never conflict (rs_apply.hpp rs_apply_lds).
-inline void nibble_tables(const uint8_t* coef_rows, int R, uint64_t out[32]) {
+// LDS nibble tables for one input shard over R output rows, entries of W bytes
+// (W = 8 for R <= 8, 16 for R <= 16): entry e (0..15) of the low table holds c_r * e in
+// byte r, entry e of the high table c_r * (e << 4); out = low[16][W] then high[16][W],
+// 32*W bytes per shard. A 16-entry table of W-byte entries spans 16*W/4 distinct LDS
+// banks (32 or all 64), so random lookups never conflict (rs_apply.hpp rs_apply_lds).
+inline int nibble_width(int R) { return R > 8 ? 16 : 8; }
+
+inline void nibble_tables(const uint8_t* coef_rows, int R, uint8_t* out) {
   const GF& g = gf();
-  for (int e = 0; e < 16; ++e) {
-    uint64_t lo = 0, hi = 0;
-    for (int r = 0; r < R && r < 8; ++r) {
-      lo |= static_cast<uint64_t>(g.mul[coef_rows[r]][e]) << (8 * r);
-      hi |= static_cast<uint64_t>(g.mul[coef_rows[r]][e << 4]) << (8 * r);
+  const int W = nibble_width(R);
+  std::memset(out, 0, static_cast<size_t>(32) * W);
+  for (int e = 0; e < 16; ++e)
+    for (int r = 0; r < R && r < W; ++r) {
+      out[e * W + r] = g.mul[coef_rows[r]][e];
+      out[(16 + e) * W + r] = g.mul[coef_rows[r]][e << 4];
     }
-    out[e] = lo;
-    out[16 + e] = hi;
-  }
 }
 
 }  // namespace callfs

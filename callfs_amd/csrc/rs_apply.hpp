@@ -262,40 +262,67 @@ void rs_apply_vec(ApplyArgs a) {
 }
 
 // ---- LDS nibble-table variant ---------------------------------------------------------
-// Per data byte two ds_read_b64 lookups (low / high nibble) return the products for all
-// RT <= 8 rows at once, so the cost per data dword is about 20 VALU + 8 LDS reads for
-// any RT, versus 5 + 4.5*RT VALU for the v_perm kernel. Tables: 256 B per input shard
-// at LDS offset 256*i (low table at +0, high at +128), loaded once per block.
-// Addresses: xl = (x << 3) & 0x78787878 holds 8*low-nibble per byte, xh the same for the
-// high nibble with bit 7 set (the +128); v_perm(base_i, xl, {j,5,6,7}) drops byte j into
-// byte 0 of the 256-B-aligned table base: one VALU per lookup.
-// Accumulation is per data-byte position (T[w][j] = 8 row products of byte j of dword w,
-// XORed over the shards); a final byte transpose (3 VALU per row) forms the row words.
+// Per data byte two LDS lookups (low / high nibble) return the products for all RT rows
+// at once (ds_read_b32 / b64 / b128 for RT <= 4 / 8 / 16), so the cost per data dword
+// is about 20-28 VALU + 8 LDS reads for any RT, versus 5 + 4.5*RT VALU for the v_perm
+// kernel. Tables (gf256.hpp nibble_tables): 32*W bytes per input shard at LDS offset
+// 32*W*i, low table first, high table at +16*W; W = 8 (RT <= 8) or 16. Loaded once
+// per block.
+// Addresses: a v_perm drops the per-byte nibble*W (precomputed for the 4 bytes of a
+// dword in one register) into byte 0 of the table base, which is 256-B aligned (W=16
+// high tables sit at +256; for W=8 the +128 of the high table is bit 7 of that byte):
+// one VALU per lookup.
+// Accumulation is per data-byte position (T[w][j] = RT row products of byte j of dword
+// w, XORed over the shards); a final byte transpose (3 VALU per row) forms row words.
+struct u32x4_acc {
+  uint32_t v[4];
+};
+
+__device__ __forceinline__ u32x4_acc operator^(const u32x4_acc& a, const u32x4_acc& b) {
+  return u32x4_acc{{a.v[0] ^ b.v[0], a.v[1] ^ b.v[1], a.v[2] ^ b.v[2], a.v[3] ^ b.v[3]}};
+}
+
 template <int RT>
 struct LdsAcc {
-  static constexpr bool WIDE = RT > 4;
-  using T = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
+  static constexpr int W = RT > 8 ? 16 : 8;  // table entry bytes
+  using T = typename std::conditional<
+      (RT > 8), u32x4_acc, typename std::conditional<(RT > 4), uint64_t, uint32_t>::type>::type;
 };
 
 template <int RT>
 __device__ __forceinline__ typename LdsAcc<RT>::T lds_lookup(const uint8_t* smem, uint32_t addr) {
-  return *reinterpret_cast<const typename LdsAcc<RT>::T*>(smem + addr);
+  using T = typename LdsAcc<RT>::T;
+  if constexpr (RT > 8) {
+    const uint4 q = *reinterpret_cast<const uint4*>(smem + addr);
+    return T{{q.x, q.y, q.z, q.w}};
+  } else {
+    return *reinterpret_cast<const T*>(smem + addr);
+  }
 }
 
 template <int RT>
 __device__ __forceinline__ void lds_mac(typename LdsAcc<RT>::T (&acc)[4][4], const uint4& x,
                                         const uint8_t* smem, uint32_t base) {
+  constexpr int W = LdsAcc<RT>::W;
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
     const uint32_t xw = word(x, w);
-    const uint32_t xl = (xw << 3) & 0x78787878u;
-    const uint32_t xh = ((xw >> 1) & 0x78787878u) | 0x80808080u;
+    uint32_t xl, xh, base_hi;
+    if constexpr (W == 8) {
+      xl = (xw << 3) & 0x78787878u;
+      xh = ((xw >> 1) & 0x78787878u) | 0x80808080u;  // +128: the high table
+      base_hi = base;
+    } else {
+      xl = (xw << 4) & 0xf0f0f0f0u;
+      xh = xw & 0xf0f0f0f0u;
+      base_hi = base + 256u;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t sel = 0x07060500u | static_cast<uint32_t>(j);
       const auto lo = lds_lookup<RT>(smem, __builtin_amdgcn_perm(base, xl, sel));
-      const auto hi = lds_lookup<RT>(smem, __builtin_amdgcn_perm(base, xh, sel));
-      acc[w][j] ^= lo ^ hi;
+      const auto hi = lds_lookup<RT>(smem, __builtin_amdgcn_perm(base_hi, xh, sel));
+      acc[w][j] = acc[w][j] ^ lo ^ hi;
     }
   }
 }
@@ -304,14 +331,16 @@ __device__ __forceinline__ void lds_mac(typename LdsAcc<RT>::T (&acc)[4][4], con
 template <int RT>
 __device__ __forceinline__ uint32_t lds_row(const typename LdsAcc<RT>::T (&t)[4], int r) {
   uint32_t t0, t1, t2, t3;
-  int rr = r;
-  if constexpr (LdsAcc<RT>::WIDE) {
+  const int rr = r & 3;
+  if constexpr (RT > 8) {
+    const int d = r >> 2;
+    t0 = t[0].v[d]; t1 = t[1].v[d]; t2 = t[2].v[d]; t3 = t[3].v[d];
+  } else if constexpr (RT > 4) {
     const int sh = r >= 4 ? 32 : 0;
     t0 = static_cast<uint32_t>(t[0] >> sh);
     t1 = static_cast<uint32_t>(t[1] >> sh);
     t2 = static_cast<uint32_t>(t[2] >> sh);
     t3 = static_cast<uint32_t>(t[3] >> sh);
-    rr = r & 3;
   } else {
     t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3];
   }
@@ -320,17 +349,24 @@ __device__ __forceinline__ uint32_t lds_row(const typename LdsAcc<RT>::T (&t)[4]
   return lo | hi;
 }
 
+template <int RT>
+__device__ __forceinline__ typename LdsAcc<RT>::T lds_zero() {
+  if constexpr (RT > 8) return typename LdsAcc<RT>::T{{0, 0, 0, 0}};
+  else return 0;
+}
+
 template <int RT, class P>
 __global__ __launch_bounds__(P::BS) __attribute__((amdgpu_waves_per_eu(P::WPE, 8)))
 void rs_apply_lds(ApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int BS = P::BS;
+  constexpr int W = LdsAcc<RT>::W;
   using AccT = typename LdsAcc<RT>::T;
   const int K = a.K;
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.ltabs);
     uint4* dst = reinterpret_cast<uint4*>(smem);
-    for (int j = threadIdx.x; j < K * 16; j += BS) dst[j] = src[j];
+    for (int j = threadIdx.x; j < K * 2 * W; j += BS) dst[j] = src[j];
   }
   __syncthreads();
   const uint32_t tps = static_cast<uint32_t>((a.nvec + BS - 1) / BS);
@@ -347,14 +383,14 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll
     for (int w = 0; w < 4; ++w)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[w][j] = 0;
+      for (int j = 0; j < 4; ++j) acc[w][j] = lds_zero<RT>();
 
     // ring of three shard vectors: shard i is consumed while i+1, i+2 load
     uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = x0;
 #pragma unroll 1
     for (int i = 0; i < K; ++i) {
       if (i + 2 < K) x2 = ld(i + 2);
-      lds_mac<RT>(acc, x0, smem, static_cast<uint32_t>(i) * 256u);
+      lds_mac<RT>(acc, x0, smem, static_cast<uint32_t>(i) * 32u * W);
       x0 = x1;
       x1 = x2;
     }
@@ -375,6 +411,9 @@ void rs_apply_lds(ApplyArgs a) {
     if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
   }
 }
+
+// Dynamic LDS bytes of rs_apply_lds for K input shards and RT rows.
+inline size_t lds_bytes(int K, int RT) { return static_cast<size_t>(K) * 32 * (RT > 8 ? 16 : 8); }
 
 // One byte position per lane over [b0, S): ragged tails and unaligned pointers.
 template <int RT>

@@ -60,7 +60,7 @@ struct Group {
   std::vector<int> shard;     // shard index per row
   uint32_t verify_mask = 0;   // bit r: compare row r (Verify) instead of storing it
   std::vector<uint32_t> tabs; // [k][R][5] v_perm tables
-  std::vector<uint64_t> ltabs;  // [k][32] LDS nibble tables (used for R >= 5)
+  std::vector<uint8_t> ltabs;  // [k][32][W] LDS nibble tables (used for R >= 5)
 };
 
 struct Tables {
@@ -94,11 +94,12 @@ std::shared_ptr<const Tables> build_tables(int k, int m, const uint8_t* present,
       for (int i = 0; i < k; ++i)
         perm_tables(dp.rows.at(row, i), &g.tabs[(static_cast<size_t>(i) * R + r) * kTabWords]);
     }
-    g.ltabs.assign(static_cast<size_t>(k) * 32, 0);
+    const size_t per_shard = 32u * nibble_width(R);
+    g.ltabs.assign(static_cast<size_t>(k) * per_shard, 0);
     for (int i = 0; i < k; ++i) {
-      uint8_t col[8] = {0};
+      uint8_t col[kMaxRowsPerLaunch] = {0};
       for (int r = 0; r < R; ++r) col[r] = dp.rows.at(g0 + r, i);
-      nibble_tables(col, R, &g.ltabs[static_cast<size_t>(i) * 32]);
+      nibble_tables(col, R, &g.ltabs[static_cast<size_t>(i) * per_shard]);
     }
     t->groups.push_back(std::move(g));
   }
@@ -190,8 +191,16 @@ struct Slot {
 };
 
 constexpr int kSlots = 3;
-// Column chunk: about this many bytes over all n shards per pipeline step.
-constexpr size_t kChunkBytes = 16u << 20;
+// Column chunk: about this many bytes over all n shards per pipeline step
+// (CALLFS_RS_CHUNK_BYTES overrides; DESIGN.md §6.3 has the sweep).
+size_t chunk_bytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("CALLFS_RS_CHUNK_BYTES");
+    const long long x = e ? std::atoll(e) : 0;
+    return x >= (64 << 10) ? static_cast<size_t>(x) : (16u << 20);
+  }();
+  return v;
+}
 
 struct Lane {
   Slot slot[kSlots];
@@ -225,7 +234,7 @@ MetaLayout meta_layout(const Tables& t, int batch) {
   for (const Group& g : t.groups) {
     L.out_off.push_back(take(sizeof(void*) * static_cast<size_t>(batch) * g.shard.size()));
     L.tab_off.push_back(take(sizeof(uint32_t) * g.tabs.size()));
-    L.ltab_off.push_back(take(sizeof(uint64_t) * g.ltabs.size()));
+    L.ltab_off.push_back(take(g.ltabs.size()));
   }
   L.total = off;
   return L;
@@ -253,7 +262,7 @@ bool fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F sh
         note(out[b * R + r]);
       }
     std::memcpy(h + L.tab_off[gi], g.tabs.data(), g.tabs.size() * sizeof(uint32_t));
-    std::memcpy(h + L.ltab_off[gi], g.ltabs.data(), g.ltabs.size() * sizeof(uint64_t));
+    std::memcpy(h + L.ltab_off[gi], g.ltabs.data(), g.ltabs.size());
   }
   return aligned;
 }
@@ -266,7 +275,7 @@ hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_
     a.in_tab = reinterpret_cast<const uint8_t* const*>(d + L.in_off);
     a.out_tab = reinterpret_cast<uint8_t* const*>(d + L.out_off[gi]);
     a.tabs = reinterpret_cast<const uint32_t*>(d + L.tab_off[gi]);
-    a.ltabs = reinterpret_cast<const uint64_t*>(d + L.ltab_off[gi]);
+    a.ltabs = d + L.ltab_off[gi];
     a.S = S;
     a.verify_mask = g.verify_mask;
     a.status = reinterpret_cast<int*>(d + L.status_off);
@@ -408,7 +417,8 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   const int out_hi = outs.empty() ? -1 : *std::max_element(outs.begin(), outs.end());
 
   size_t cw = S;  // chunk width (bytes per shard), a multiple of 4 KiB unless one chunk
-  if (S * n > kChunkBytes) cw = std::max<size_t>(4096, kChunkBytes / n / 4096 * 4096);
+  const size_t cb = chunk_bytes();
+  if (S * n > cb) cw = std::max<size_t>(4096, cb / n / 4096 * 4096);
   const size_t cpitch = round_up(cw, kPitchAlign);
   const size_t nchunks = (S + cw - 1) / cw;
   const int nslots = static_cast<int>(std::min<size_t>(nchunks, kSlots));

@@ -3,6 +3,7 @@
 // on MI355X (DESIGN.md "Kernel tuning log").
 #include <algorithm>
 #include <array>
+#include <mutex>
 #include <utility>
 
 #include "rs_apply.hpp"
@@ -20,11 +21,12 @@ using dev::kBlock;
 // 5957 GB/s for an XOR-only kernel with the same loads and stores.
 using ProdPolicy = dev::Policy<4, 1, true, true, false, 512, 2, 0>;
 
-// Row groups of 5..8 use the LDS nibble-table kernel: its cost does not grow with the
+// Row groups of 5..16 use the LDS nibble-table kernel: its cost does not grow with the
 // row count (RS(10,8): 5,749 vs 4,887 GB/s; RS(32,8): 4,783 vs 3,948; RS(12,6): 5,318
 // vs 5,118 — tools/kbench.hip), while for R <= 4 the v_perm kernel is faster.
 using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
 constexpr int kLdsMinRows = 5;
+constexpr int kPermMaxRows = 8;  // v_perm kernel instantiations (production uses <= 4)
 
 using VecFn = void (*)(ApplyArgs);
 using ByteFn = void (*)(ApplyArgs, uint64_t);
@@ -44,7 +46,7 @@ constexpr auto byte_table(std::integer_sequence<int, Rs...>) {
   return std::array<ByteFn, sizeof...(Rs)>{&dev::rs_apply_bytes<Rs + 1>...};
 }
 
-const auto kVec = vec_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
+const auto kVec = vec_table(std::make_integer_sequence<int, kPermMaxRows>{});
 const auto kLds = lds_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
@@ -59,9 +61,19 @@ hipError_t launch_apply(ApplyArgs a, bool aligned, hipStream_t stream) {
     a.nvec = a.S / 16;
     tail0 = a.nvec * 16;
     if (a.nvec) {
-      if (a.R >= kLdsMinRows && a.ltabs) {
+      if (a.R >= kLdsMinRows || a.R > kPermMaxRows) {
+        if (!a.ltabs) return hipErrorInvalidValue;
+        const size_t lds = dev::lds_bytes(a.K, a.R);
+        VecFn fn = kLds[a.R - 1];
+        if (lds > (64u << 10)) {  // wide groups with many shards: opt in once per kernel
+          static std::once_flag once[kMaxRowsPerLaunch];
+          std::call_once(once[a.R - 1], [fn] {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
+          });
+        }
         const unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
-        hipLaunchKernelGGL(kLds[a.R - 1], dim3(gx), dim3(LdsPolicy::BS), a.K * 256, stream, a);
+        hipLaunchKernelGGL(fn, dim3(gx), dim3(LdsPolicy::BS), lds, stream, a);
       } else {
         const unsigned gx = dev::vec_grid<ProdPolicy>(a.nvec, a.batch);
         hipLaunchKernelGGL(kVec[a.R - 1], dim3(gx), dim3(ProdPolicy::BS), 0, stream, a);

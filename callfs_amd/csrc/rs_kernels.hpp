@@ -6,7 +6,7 @@
 
 namespace callfs {
 
-constexpr int kMaxRowsPerLaunch = 8;  // output rows held in registers per launch
+constexpr int kMaxRowsPerLaunch = 16;  // output rows per launch group (LDS kernel above 4)
 constexpr int kMaxK = 256;
 
 // One launch applies an R x K coefficient block to every stripe of a batch:
@@ -17,7 +17,7 @@ struct ApplyArgs {
   const uint8_t* const* in_tab;  // [batch][K] device pointers (k valid shards)
   uint8_t* const* out_tab;       // [batch][R] device pointers (written or compared)
   const uint32_t* tabs;          // [K][R][5] v_perm tables (gf256.hpp perm_tables)
-  const uint64_t* ltabs;         // [K][32] nibble tables for rs_apply_lds (gf256.hpp nibble_tables)
+  const uint8_t* ltabs;          // [K][32][W] nibble tables for rs_apply_lds (gf256.hpp nibble_tables)
   uint64_t S;                    // shard bytes
   uint64_t nvec;                 // 16-byte vectors per shard handled by the vector kernel
   uint32_t verify_mask;

@@ -73,6 +73,62 @@ int main() {
         CHECK(((p >> (8 * b)) & 0xff) == g.mul[c][(x >> (8 * b)) & 0xff]);
     }
   }
+  // 2b. LDS nibble-table kernel math (rs_apply.hpp lds_mac / lds_row) emulated on the
+  // CPU: table layout, v_perm address formation (W = 8 and 16), per-position
+  // accumulation and the final byte transpose, for R = 1..16 rows and K = 3 shards.
+  for (int R = 1; R <= 16; ++R) {
+    const int K = 3, W = nibble_width(R);
+    std::mt19937 rng(R);
+    std::vector<uint8_t> coef(static_cast<size_t>(K) * R);
+    for (auto& c : coef) c = static_cast<uint8_t>(rng());
+    std::vector<uint8_t> lds(static_cast<size_t>(K) * 32 * W);
+    for (int i = 0; i < K; ++i) {
+      uint8_t col[16] = {0};
+      for (int r = 0; r < R; ++r) col[r] = coef[static_cast<size_t>(r) * K + i];
+      nibble_tables(col, R, &lds[static_cast<size_t>(i) * 32 * W]);
+    }
+    for (int trial = 0; trial < 64; ++trial) {
+      uint32_t x[3];
+      for (auto& v : x) v = static_cast<uint32_t>(rng());
+      uint8_t T[4][16] = {};  // per byte position j: products for all rows
+      for (int i = 0; i < K; ++i) {
+        const uint32_t base = static_cast<uint32_t>(i) * 32u * W;
+        uint32_t xl, xh, base_hi;
+        if (W == 8) {
+          xl = (x[i] << 3) & 0x78787878u;
+          xh = ((x[i] >> 1) & 0x78787878u) | 0x80808080u;
+          base_hi = base;
+        } else {
+          xl = (x[i] << 4) & 0xf0f0f0f0u;
+          xh = x[i] & 0xf0f0f0f0u;
+          base_hi = base + 256u;
+        }
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t sel = 0x07060500u | static_cast<uint32_t>(j);
+          const uint32_t alo = v_perm(base, xl, sel), ahi = v_perm(base_hi, xh, sel);
+          for (int b = 0; b < W; ++b) T[j][b] ^= lds[alo + b] ^ lds[ahi + b];
+        }
+      }
+      for (int r = 0; r < R; ++r) {
+        // lds_row: byte r of T[0..3] via two v_perm on the dwords holding row r
+        auto dw = [&](int j) {
+          const int d = r >> 2;
+          return static_cast<uint32_t>(T[j][4 * d]) | (static_cast<uint32_t>(T[j][4 * d + 1]) << 8) |
+                 (static_cast<uint32_t>(T[j][4 * d + 2]) << 16) | (static_cast<uint32_t>(T[j][4 * d + 3]) << 24);
+        };
+        const int rr = r & 3;
+        const uint32_t lo = v_perm(dw(1), dw(0), 0x0c0c0400u | (0x0101u * rr));
+        const uint32_t hi = v_perm(dw(3), dw(2), 0x04000c0cu | (0x01010000u * rr));
+        const uint32_t got = lo | hi;
+        for (int j = 0; j < 4; ++j) {
+          uint8_t want = 0;
+          for (int i = 0; i < K; ++i)
+            want ^= g.mul[coef[static_cast<size_t>(r) * K + i]][(x[i] >> (8 * j)) & 0xff];
+          CHECK(((got >> (8 * j)) & 0xff) == want);
+        }
+      }
+    }
+  }
   // 3. decode rows: every erasure pattern of RS(6,3) up to 3 erasures
   {
     const int k = 6, m = 3, n = 9, S = 64;

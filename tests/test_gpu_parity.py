@@ -125,10 +125,11 @@ def test_golden_fixtures(codec):
         assert got == case["shard_sha256"], case["name"]
 
 
-# R = m rows per launch group: 1..4 take the v_perm kernel, 5..8 the LDS nibble-table
-# kernel, m > 8 splits into several groups (9 = 8+1, 10 = 8+2, 20 = 8+8+4).
+# R = m rows per launch group: 1..4 take the v_perm kernel, 5..8 the LDS kernel with
+# 8-byte nibble entries, 9..16 with 16-byte entries; m > 16 splits (20 = 16+4).
 PROFILES = [(1, 1), (2, 1), (3, 2), (4, 2), (5, 5), (6, 3), (8, 4), (10, 4), (12, 4),
-            (16, 4), (17, 3), (10, 6), (12, 7), (20, 10), (32, 8), (6, 9), (40, 20)]
+            (16, 4), (17, 3), (10, 6), (12, 7), (20, 10), (32, 8), (6, 9), (4, 13),
+            (10, 12), (12, 16), (40, 20)]
 
 
 @pytest.mark.parametrize("k,m", PROFILES)
@@ -342,6 +343,23 @@ def test_full_size_config_rs10_4_64mib_roundtrip(native_lib):
         assert torch.equal(sb.buf[:, :, :S], ref[:, :, :S]), erase
 
 
+@pytest.mark.parametrize("erase_n", [9, 12, 16])
+def test_decode_wide_erasures(codec, erase_n):
+    """9..16 erased shards in one launch group (LDS kernel, 16-byte nibble entries)."""
+    from callfs_amd import ErasureProfile
+    k, m = 20, 16
+    L = 3 * 1024 * 1024 + 5
+    data = rnd(erase_n, L)
+    full = [bytes(s) for s in codec.encode(data, ErasureProfile(k, m))]
+    want = oracle_shards(data, k, m)
+    assert all(f == w.tobytes() for f, w in zip(full, want))
+    rng = np.random.default_rng(erase_n)
+    erase = set(rng.choice(k + m, size=erase_n, replace=False).tolist())
+    shards = [None if i in erase else full[i] for i in range(k + m)]
+    assert codec.decode(shards, ErasureProfile(k, m), L) == data
+    assert all(bytes(shards[i]) == full[i] for i in erase)
+
+
 @pytest.mark.parametrize("k,m", [(200, 56), (255, 1), (128, 128), (1, 255)])
 def test_max_profiles_roundtrip(codec, k, m):
     """k+m = 256 is the largest GF(2^8) profile (upstream switches to Leopard above)."""
@@ -402,3 +420,37 @@ def test_small_objects_concurrent(codec):
     for t in ts:
         t.join()
     assert not errors, errors[:3]
+
+
+def test_empty_and_zero_length_edges(codec):
+    """Split of an empty object fails like upstream (codec.go:31-34 -> ErrShortData);
+    Decode with originalSize 0 returns an empty buffer after reconstruct+verify."""
+    from callfs_amd import ErasureProfile, ErrShortData
+    p = ErasureProfile(4, 2)
+    with pytest.raises(ErrShortData) as ei:
+        codec.encode(b"", p)
+    assert str(ei.value) == ("erasure: failed to split data: not enough data to fill the "
+                             "number of requested shards")
+    sh = [bytes(s) for s in codec.encode(b"abc", p)]
+    assert codec.decode([None] + sh[1:], p, 0) == b""
+
+
+def test_one_gib_object_roundtrip(native_lib):
+    """configs[3] object size: RS(10,4) over a 1 GiB object (S = 107,374,183, a 7-byte
+    ragged tail), two objects, encode + worst-case decode, bit-exact on device; the first
+    and last 1 MiB of object 0's parity checked against the oracle."""
+    import torch
+    from callfs_amd.device import Plan
+    k, m, S, batch = 10, 4, 107_374_183, 2
+    sb = _batch(k, m, S, batch, seed=1 << 30)
+    Plan.for_batch(sb).launch()
+    ref = sb.buf[:, :, :S].clone()
+    for sl in (slice(0, 1 << 20), slice(S - (1 << 20), S)):
+        host = sb.buf[0, :, sl].cpu().numpy()
+        want = cref.encode([host[i] for i in range(k)], k, m)
+        assert all(np.array_equal(host[k + j], want[j]) for j in range(m))
+    sb.buf[:, :4, :S].zero_()
+    dec = Plan.for_batch(sb, present=[i >= 4 for i in range(14)])
+    dec.launch()
+    assert not dec.corrupt()
+    assert torch.equal(sb.buf[:, :, :S], ref)

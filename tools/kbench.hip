@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void xor_stream(ApplyArgs a) {
 template <int R, class P>
 void launch_lds(const ApplyArgs& a, hipStream_t s) {
   const unsigned g = static_cast<unsigned>((a.nvec + P::BS - 1) / P::BS * a.batch);
-  hipLaunchKernelGGL((dev::rs_apply_lds<R, P>), dim3(g), dim3(P::BS), a.K * 256, s, a);
+  hipLaunchKernelGGL((dev::rs_apply_lds<R, P>), dim3(g), dim3(P::BS), dev::lds_bytes(a.K, R), s, a);
 }
 
 // Read-only ceiling: the K input streams, nothing stored unless an impossible value.
@@ -127,8 +127,8 @@ int main(int argc, char** argv) {
   const int rounds = argc > 5 ? std::atoi(argv[5]) : 5;
   const int iters = argc > 6 ? std::atoi(argv[6]) : 10;
   const size_t palign = argc > 7 ? std::strtoull(argv[7], nullptr, 0) : 256;
-  if (m < 1 || m > 8 || k < 1 || k > 256) {
-    std::fprintf(stderr, "need 1<=m<=8, 1<=k<=256\n");
+  if (m < 1 || m > 16 || k < 1 || k > 256) {
+    std::fprintf(stderr, "need 1<=m<=16, 1<=k<=256\n");
     return 2;
   }
   const int n = k + m;
@@ -147,11 +147,12 @@ int main(int argc, char** argv) {
   std::vector<uint32_t> tabs(static_cast<size_t>(k) * m * 5);
   for (int i = 0; i < k; ++i)
     for (int r = 0; r < m; ++r) perm_tables(E.at(k + r, i), &tabs[(static_cast<size_t>(i) * m + r) * 5]);
-  std::vector<uint64_t> ltabs(static_cast<size_t>(k) * 32);
+  const size_t lper = 32u * nibble_width(m);
+  std::vector<uint8_t> ltabs(static_cast<size_t>(k) * lper);
   for (int i = 0; i < k; ++i) {
-    uint8_t col[8] = {0};
-    for (int r = 0; r < m && r < 8; ++r) col[r] = E.at(k + r, i);
-    nibble_tables(col, m, &ltabs[static_cast<size_t>(i) * 32]);
+    uint8_t col[16] = {0};
+    for (int r = 0; r < m && r < 16; ++r) col[r] = E.at(k + r, i);
+    nibble_tables(col, m, &ltabs[static_cast<size_t>(i) * lper]);
   }
   std::vector<const uint8_t*> in(static_cast<size_t>(B) * k);
   std::vector<uint8_t*> out(static_cast<size_t>(B) * m);
@@ -164,8 +165,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_in, in.size() * sizeof(void*)));
   CK(hipMalloc(&d_out, out.size() * sizeof(void*)));
   CK(hipMalloc(&d_tabs, tabs.size() * 4));
-  CK(hipMalloc(&d_ltabs, ltabs.size() * 8));
-  CK(hipMemcpy(d_ltabs, ltabs.data(), ltabs.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMalloc(&d_ltabs, ltabs.size()));
+  CK(hipMemcpy(d_ltabs, ltabs.data(), ltabs.size(), hipMemcpyHostToDevice));
   CK(hipMalloc(&d_status, 4));
   CK(hipMemcpy(d_in, in.data(), in.size() * sizeof(void*), hipMemcpyHostToDevice));
   CK(hipMemcpy(d_out, out.data(), out.size() * sizeof(void*), hipMemcpyHostToDevice));
@@ -176,7 +177,7 @@ int main(int argc, char** argv) {
   a.in_tab = static_cast<const uint8_t* const*>(d_in);
   a.out_tab = static_cast<uint8_t* const*>(d_out);
   a.tabs = static_cast<const uint32_t*>(d_tabs);
-  a.ltabs = static_cast<const uint64_t*>(d_ltabs);
+  a.ltabs = static_cast<const uint8_t*>(d_ltabs);
   a.S = S;
   a.nvec = S / 16;
   a.verify_mask = 0;
@@ -219,6 +220,12 @@ int main(int argc, char** argv) {
       break;
     case 6:
       vs.push_back(Variant{"lds bs512", [](const ApplyArgs& a, hipStream_t s) { launch_lds<6, L512>(a, s); }});
+      break;
+    case 12:
+      vs.push_back(Variant{"lds b128 (prod R 9..16)", [](const ApplyArgs& a, hipStream_t s) { launch_lds<12, L512w2>(a, s); }});
+      break;
+    case 16:
+      vs.push_back(Variant{"lds b128 (prod R 9..16)", [](const ApplyArgs& a, hipStream_t s) { launch_lds<16, L512w2>(a, s); }});
       break;
   }
   if (rs10_4) vs.push_back(Variant{"read-only 10 streams (bytes: 10/14)", [](const ApplyArgs& a, hipStream_t s) {
