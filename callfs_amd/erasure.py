@@ -143,31 +143,34 @@ class Codec:
         return self._ctx
 
     def encode(self, data, profile: ErasureProfile) -> List[memoryview]:
-        """codec.go:21-41. Returns data_shards+parity_shards equal-length shards (the
-        data is zero-padded to k*S, S = ceil(len/k)); they are views into one buffer,
-        the way upstream Split aliases the input."""
+        """codec.go:21-41. Returns data_shards+parity_shards equal-length shards: S =
+        ceil(len/k); like upstream Split the full data shards are views into `data`
+        (no copy), the shard holding the end of the object and any after it are
+        zero-padded copies, and only the m parity shards are computed (rs_encode)."""
         k, m = profile.data_shards, profile.parity_shards
         if k < 1 or m < 1:
             raise ErrInvalidProfile()
-        src = memoryview(data).cast("B") if not isinstance(data, (bytes, bytearray)) else data
+        if k + m > 256:
+            raise _wrapped(N.RS_E_UNSUPPORTED, "erasure: failed to create encoder")
+        src = memoryview(data).cast("B")
         L = len(src)
         if L == 0:
             raise ErrShortData(f"erasure: failed to split data: {ErrShortData.text}")
         S = (L + k - 1) // k
-        out = bytearray(S * (k + m))
-        ss = ctypes.c_size_t(0)
-        rc = N.lib.rs_codec_encode(self.context.handle, k, m, _addr(src), L,
-                                   _addr(out), len(out), ctypes.byref(ss))
-        if rc == N.RS_E_INVALID_PROFILE:
-            raise ErrInvalidProfile()
-        if rc == N.RS_E_SHORT_DATA:
-            raise _wrapped(rc, "erasure: failed to split data")
-        if rc == N.RS_E_UNSUPPORTED:
-            raise _wrapped(rc, "erasure: failed to create encoder")
+        full = L // S  # data shards lying entirely inside `data`
+        tail = bytearray(S * (k - full))
+        tail[: L - full * S] = src[full * S:]
+        parity = bytearray(S * m)
+        tv, pv = memoryview(tail), memoryview(parity)
+        shards = [src[i * S:(i + 1) * S] for i in range(full)]
+        shards += [tv[i * S:(i + 1) * S] for i in range(k - full)]
+        shards += [pv[j * S:(j + 1) * S] for j in range(m)]
+        dptr = (ctypes.c_void_p * k)(*[_addr(s) for s in shards[:k]])
+        pptr = (ctypes.c_void_p * m)(*[_addr(s) for s in shards[k:]])
+        rc = N.lib.rs_encode(self.context.handle, k, m, S, dptr, pptr)
         if rc != N.RS_OK:
             raise _wrapped(rc, "erasure: failed to encode parity")
-        mv = memoryview(out)
-        return [mv[i * S:(i + 1) * S] for i in range(k + m)]
+        return shards
 
     def decode(self, shards: List, profile: ErasureProfile, original_size: int) -> bytearray:
         """codec.go:45-78. `None` or empty entries are missing shards; they are

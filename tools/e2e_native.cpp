@@ -5,6 +5,8 @@
 // build: g++ -O2 -std=c++17 -I include tools/e2e_native.cpp -L callfs_amd -lcallfs_rs \
 //          -Wl,-rpath,'$ORIGIN/../callfs_amd' -lpthread -o tools/e2e_native
 // run:   tools/e2e_native k m object_bytes threads seconds [erase,list]
+// CALLFS_E2E_ENCODER=1: encode through rs_encode (Go-side Split aliasing the object,
+// parity only, as INTEGRATION.md's shim does) instead of rs_codec_encode.
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -36,6 +38,7 @@ int main(int argc, char** argv) {
       p = q + 1;
     }
   }
+  const bool encoder_api = std::getenv("CALLFS_E2E_ENCODER") != nullptr;
   rs_ctx* ctx = nullptr;
   if (rs_init(&ctx, 0) != RS_OK) {
     std::fprintf(stderr, "rs_init failed\n");
@@ -72,7 +75,23 @@ int main(int argc, char** argv) {
         std::vector<size_t> lens(n);
         while (!stop.load(std::memory_order_relaxed)) {
           int rc;
-          if (encode) {
+          if (encode && encoder_api) {
+            // Split as upstream: full data shards alias src, the tail shard is a
+            // zero-padded copy, parity lands in fresh buffers
+            const size_t full = L / S;
+            std::vector<const uint8_t*> dptr(k);
+            std::vector<uint8_t*> pptr(m);
+            for (size_t i = 0; i < full; ++i) dptr[i] = me.src.data() + S * i;
+            for (int i = static_cast<int>(full); i < k; ++i) {
+              uint8_t* t = enc2.data() + S * i;
+              const size_t have = i == static_cast<int>(full) ? L - full * S : 0;
+              std::memcpy(t, me.src.data() + full * S, have);
+              std::memset(t + have, 0, S - have);
+              dptr[i] = t;
+            }
+            for (int j = 0; j < m; ++j) pptr[j] = enc2.data() + S * (k + j);
+            rc = rs_encode(ctx, k, m, S, dptr.data(), pptr.data());
+          } else if (encode) {
             size_t ss = 0;
             rc = rs_codec_encode(ctx, k, m, me.src.data(), L, enc2.data(), n * S, &ss);
           } else {
@@ -105,10 +124,10 @@ int main(int argc, char** argv) {
   auto d = run(false);
   int bad = 0;
   for (auto& x : th) bad |= x.err || x.out != x.src;
-  std::printf("{\"api\": \"native\", \"k\": %d, \"m\": %d, \"object_bytes\": %zu, \"threads\": %d, "
+  std::printf("{\"api\": \"%s\", \"k\": %d, \"m\": %d, \"object_bytes\": %zu, \"threads\": %d, "
               "\"erase_count\": %zu, \"encode_gib_s\": %.3f, \"decode_gib_s\": %.3f, "
               "\"encode_calls\": %ld, \"decode_calls\": %ld, \"ok\": %s}\n",
-              k, m, L, T, erase.size(), e.first, d.first, e.second, d.second, bad ? "false" : "true");
+              encoder_api ? "native-encoder" : "native", k, m, L, T, erase.size(), e.first, d.first, e.second, d.second, bad ? "false" : "true");
   rs_shutdown(ctx);
   return bad ? 1 : 0;
 }
