@@ -67,6 +67,10 @@ SIGNATURES = {
     "rs_reconstruct": (_int, [_vp, _int, _int, ctypes.POINTER(_vp), ctypes.POINTER(_sz)]),
     "rs_verify": (_int, [_vp, _int, _int, ctypes.POINTER(_vp), ctypes.POINTER(_sz),
                          ctypes.POINTER(_int)]),
+    "rs_encode_batch": (_int, [_vp, _int, _int, _int, ctypes.POINTER(_sz), ctypes.POINTER(_vp),
+                               ctypes.POINTER(_vp), ctypes.POINTER(_int)]),
+    "rs_reconstruct_batch": (_int, [_vp, _int, _int, _int, ctypes.POINTER(_vp), ctypes.POINTER(_sz),
+                                    _int, ctypes.POINTER(_int)]),
     "rs_plan_create": (_int, [_vp, _int, _int, _int, _sz, _int, _u8p, ctypes.POINTER(_vp),
                               ctypes.POINTER(_vp)]),
     "rs_plan_launch": (_int, [_vp, _vp]),

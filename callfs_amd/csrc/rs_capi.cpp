@@ -21,6 +21,7 @@
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -185,9 +186,12 @@ struct Slot {
   HostBuf hmeta;
   std::shared_ptr<const Tables> meta_tables;  // what `meta` currently holds
   size_t meta_pitch = 0;
+  int meta_spc = 0;
   void* meta_base = nullptr;
+  HostBuf hstat;         // per-stripe verify flags of the chunk in flight
   bool pending = false;  // a chunk's outputs wait in `host`
-  size_t off = 0, width = 0;
+  int b0 = 0, count = 0;  // its stripes
+  size_t off = 0, width = 0;  // and columns
 };
 
 constexpr int kSlots = 3;
@@ -204,7 +208,6 @@ size_t chunk_bytes() {
 
 struct Lane {
   Slot slot[kSlots];
-  HostBuf hstatus;  // pinned status words read back at the end of a call
 };
 
 struct Device {
@@ -314,10 +317,10 @@ struct rs_ctx {
           sl.host.release();
           sl.meta.release();
           sl.hmeta.release();
+          sl.hstat.release();
           if (sl.done) (void)hipEventDestroy(sl.done);
           if (sl.stream) (void)hipStreamDestroy(sl.stream);
         }
-        l->hstatus.release();
       }
 
     }
@@ -344,7 +347,6 @@ struct rs_ctx {
           if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess ||
               hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
             return nullptr;
-        if (l->hstatus.ensure(kSlots * sizeof(int))) return nullptr;
         d->lanes.push_back(std::move(l));
         return d->lanes.back().get();
       }
@@ -372,25 +374,30 @@ struct LaneGuard {
   }
 };
 
-// Host-memory path (Codec.Encode/Decode ends, codec.go:21-78): the shard columns
-// [0, S) are cut into chunks that rotate through the lane's kSlots slots. Per chunk:
-// copy-pool copies of the input shards' columns into pinned memory, H2D, the kernel
-// groups, D2H of the written shards on the slot's stream; the CPU copies chunk j in
-// while the GPU/DMA work on chunks j-1 and j-2, and copies chunk j-kSlots out.
-// in(i)/out(i) give host buffers by shard index. Returns RS_OK, RS_E_CORRUPT (verify
-// rows mismatched) or an error.
+// Host-memory path (Codec.Encode/Decode ends, codec.go:21-78) over `batch` stripes that
+// share one table set and one shard size S. Work is cut into chunks that rotate through
+// the lane's kSlots slots: a chunk is a block of whole stripes when a stripe is small
+// (many stripes per H2D / launch / D2H), otherwise one column range [off, off+w) of a
+// single stripe. Per chunk: copy-pool copies of the input shards into pinned memory
+// ([stripe][n][cpitch]), H2D, the kernel groups, D2H of the written shards (and of the
+// per-stripe status words when there are verify rows) on the slot's stream; the CPU
+// copies chunk j in while the GPU/DMA work on chunks j-1 and j-2, and copies chunk
+// j-kSlots out. in(b, i)/out(b, i) give host buffers by stripe and shard index.
+// stripe_status (nullable, `batch` ints) receives 1 for stripes whose verify rows
+// mismatched. Returns RS_OK, RS_E_CORRUPT (some stripe mismatched) or an error.
 template <class InF, class OutF>
 int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const Tables>& tp,
-                  size_t S, InF host_in, OutF host_out);
+                  size_t S, int batch, InF host_in, OutF host_out, int* stripe_status);
 
 template <class InF, class OutF>
-int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, InF host_in,
-             OutF host_out) {
+int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, int batch,
+             InF host_in, OutF host_out, int* stripe_status = nullptr) {
   if (ctx->devs.empty()) return RS_E_HIP;
   Device* dev = ctx->devs[ctx->rr.fetch_add(1) % ctx->devs.size()].get();
   LaneGuard lg{ctx, dev, ctx->acquire(dev)};
   if (!lg.lane) return RS_E_HIP;
-  const int rc = run_host_impl(ctx, *lg.lane, dev->id, tp, S, host_in, host_out);
+  const int rc =
+      run_host_impl(ctx, *lg.lane, dev->id, tp, S, batch, host_in, host_out, stripe_status);
   if (rc != RS_OK && rc != RS_E_CORRUPT) {
     // never hand a lane with work in flight to the next caller
     for (Slot& sl : lg.lane->slot) {
@@ -401,12 +408,20 @@ int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, InF
   return rc;
 }
 
+// Single-stripe form used by the per-object entry points.
+template <class InF, class OutF>
+int run_host1(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, InF in, OutF out) {
+  return run_host(ctx, tp, S, 1, [&](int, int i) { return in(i); },
+                  [&](int, int i) { return out(i); });
+}
+
 template <class InF, class OutF>
 int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const Tables>& tp,
-                  size_t S, InF host_in, OutF host_out) {
+                  size_t S, int batch, InF host_in, OutF host_out, int* stripe_status) {
   const Tables& t = *tp;
   HIPCHK(hipSetDevice(device));
   const int n = t.k + t.m;
+  const bool verify = !t.check.empty();
 
   std::vector<int> ins(t.valid);
   ins.insert(ins.end(), t.check.begin(), t.check.end());
@@ -416,82 +431,118 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   const int out_lo = outs.empty() ? 0 : *std::min_element(outs.begin(), outs.end());
   const int out_hi = outs.empty() ? -1 : *std::max_element(outs.begin(), outs.end());
 
-  size_t cw = S;  // chunk width (bytes per shard), a multiple of 4 KiB unless one chunk
+  // chunk shape: cw bytes per shard (a multiple of 4 KiB unless the whole shard) and
+  // spc stripes per chunk (>1 only when a whole stripe fits several times in a chunk)
+  size_t cw = S;
+  int spc = 1;
   const size_t cb = chunk_bytes();
-  if (S * n > cb) cw = std::max<size_t>(4096, cb / n / 4096 * 4096);
+  if (S * n > cb) {
+    cw = std::max<size_t>(4096, cb / n / 4096 * 4096);
+  } else {
+    const size_t per = round_up(S, kPitchAlign) * n;
+    spc = static_cast<int>(std::min<size_t>(static_cast<size_t>(batch), std::max<size_t>(1, cb / per)));
+  }
   const size_t cpitch = round_up(cw, kPitchAlign);
-  const size_t nchunks = (S + cw - 1) / cw;
+  const size_t spitch = cpitch * n;  // one stripe in a slot's staging buffer
+  const size_t ncol = (S + cw - 1) / cw;
+  const size_t nblk = (static_cast<size_t>(batch) + spc - 1) / spc;
+  const size_t nchunks = ncol * nblk;
   const int nslots = static_cast<int>(std::min<size_t>(nchunks, kSlots));
-  const MetaLayout ML = meta_layout(t, 1);
-  // small chunks move as one contiguous row range instead of one copy per shard
-  const bool coalesce = cpitch * n <= (4u << 20);
+  const MetaLayout ML = meta_layout(t, spc);
+  // small stripes move as one contiguous row range instead of one copy per shard
+  const bool coalesce = spitch <= (4u << 20);
 
   for (int si = 0; si < nslots; ++si) {
     Slot& sl = L.slot[si];
     int rc;
-    if ((rc = sl.dev.ensure(cpitch * n)) || (rc = sl.host.ensure(cpitch * n)) ||
-        (rc = sl.meta.ensure(ML.total)) || (rc = sl.hmeta.ensure(ML.total)))
+    if ((rc = sl.dev.ensure(spitch * spc)) || (rc = sl.host.ensure(spitch * spc)) ||
+        (rc = sl.meta.ensure(ML.total)) || (rc = sl.hmeta.ensure(ML.total)) ||
+        (rc = sl.hstat.ensure(sizeof(int) * spc)))
       return rc;
-    if (sl.meta_tables != tp || sl.meta_pitch != cpitch || sl.meta_base != sl.dev.p) {
+    if (sl.meta_tables != tp || sl.meta_pitch != cpitch || sl.meta_spc != spc ||
+        sl.meta_base != sl.dev.p) {
       auto* base = static_cast<uint8_t*>(sl.dev.p);
-      fill_meta(t, ML, 1, static_cast<uint8_t*>(sl.hmeta.p),
-                [&](int, int i) { return base + cpitch * i; });
+      fill_meta(t, ML, spc, static_cast<uint8_t*>(sl.hmeta.p),
+                [&](int b, int i) { return base + spitch * b + cpitch * i; });
       HIPCHK(hipMemcpyAsync(sl.meta.p, sl.hmeta.p, ML.total, hipMemcpyHostToDevice, sl.stream));
       sl.meta_tables = tp;
       sl.meta_pitch = cpitch;
+      sl.meta_spc = spc;
       sl.meta_base = sl.dev.p;
-    } else {
-      HIPCHK(hipMemsetAsync(static_cast<uint8_t*>(sl.meta.p) + ML.status_off, 0, sizeof(int),
-                            sl.stream));
     }
     sl.pending = false;
   }
 
+  bool corrupt = false;
   std::vector<CopyPool::Seg> segs;
   auto drain = [&](Slot& sl) -> int {
     if (!sl.pending) return RS_OK;
     HIPCHK(hipEventSynchronize(sl.done));
     segs.clear();
     auto* h = static_cast<uint8_t*>(sl.host.p);
-    for (int i : outs) segs.push_back({host_out(i) + sl.off, h + cpitch * i, sl.width});
+    for (int b = 0; b < sl.count; ++b)
+      for (int i : outs)
+        segs.push_back({host_out(sl.b0 + b, i) + sl.off, h + spitch * b + cpitch * i, sl.width});
     ctx->pool.run(segs);
+    if (verify) {
+      const int* st = static_cast<const int*>(sl.hstat.p);
+      for (int b = 0; b < sl.count; ++b)
+        if (st[b]) {
+          corrupt = true;
+          if (stripe_status) stripe_status[sl.b0 + b] = 1;
+        }
+    }
     sl.pending = false;
     return RS_OK;
   };
 
+  int* dstatus = nullptr;
   for (size_t j = 0; j < nchunks; ++j) {
     Slot& sl = L.slot[j % kSlots];
     int rc = drain(sl);
     if (rc) return rc;
-    const size_t off = j * cw, w = std::min(cw, S - off);
+    const int b0 = static_cast<int>(j / ncol) * spc;
+    const int cnt = std::min(spc, batch - b0);
+    const size_t off = (j % ncol) * cw, w = std::min(cw, S - off);
     auto* h = static_cast<uint8_t*>(sl.host.p);
     auto* d = static_cast<uint8_t*>(sl.dev.p);
+    auto* meta = static_cast<uint8_t*>(sl.meta.p);
+    dstatus = reinterpret_cast<int*>(meta + ML.status_off);
     segs.clear();
-    for (int i : ins) segs.push_back({h + cpitch * i, host_in(i) + off, w});
+    for (int b = 0; b < cnt; ++b)
+      for (int i : ins) segs.push_back({h + spitch * b + cpitch * i, host_in(b0 + b, i) + off, w});
     ctx->pool.run(segs);
     if (coalesce) {
-      const size_t bytes = cpitch * (in_hi - in_lo) + w;
+      const size_t bytes = spitch * (cnt - 1) + cpitch * (in_hi - in_lo) + w;
       HIPCHK(hipMemcpyAsync(d + cpitch * in_lo, h + cpitch * in_lo, bytes,
                             hipMemcpyHostToDevice, sl.stream));
     } else {
-      for (int i : ins)
-        HIPCHK(hipMemcpyAsync(d + cpitch * i, h + cpitch * i, w, hipMemcpyHostToDevice,
-                              sl.stream));
+      for (int b = 0; b < cnt; ++b)
+        for (int i : ins)
+          HIPCHK(hipMemcpyAsync(d + spitch * b + cpitch * i, h + spitch * b + cpitch * i, w,
+                                hipMemcpyHostToDevice, sl.stream));
     }
-    HIPCHK(launch_groups(t, ML, 1, static_cast<uint8_t*>(sl.meta.p), w, true, sl.stream));
+    if (verify) HIPCHK(hipMemsetAsync(dstatus, 0, sizeof(int) * cnt, sl.stream));
+    HIPCHK(launch_groups(t, ML, cnt, meta, w, true, sl.stream, 1));
     if (!outs.empty()) {
       if (coalesce) {
-        const size_t bytes = cpitch * (out_hi - out_lo) + w;
+        const size_t bytes = spitch * (cnt - 1) + cpitch * (out_hi - out_lo) + w;
         HIPCHK(hipMemcpyAsync(h + cpitch * out_lo, d + cpitch * out_lo, bytes,
                               hipMemcpyDeviceToHost, sl.stream));
       } else {
-        for (int i : outs)
-          HIPCHK(hipMemcpyAsync(h + cpitch * i, d + cpitch * i, w, hipMemcpyDeviceToHost,
-                                sl.stream));
+        for (int b = 0; b < cnt; ++b)
+          for (int i : outs)
+            HIPCHK(hipMemcpyAsync(h + spitch * b + cpitch * i, d + spitch * b + cpitch * i, w,
+                                  hipMemcpyDeviceToHost, sl.stream));
       }
     }
+    if (verify)
+      HIPCHK(hipMemcpyAsync(sl.hstat.p, dstatus, sizeof(int) * cnt, hipMemcpyDeviceToHost,
+                            sl.stream));
     HIPCHK(hipEventRecord(sl.done, sl.stream));
     sl.pending = true;
+    sl.b0 = b0;
+    sl.count = cnt;
     sl.off = off;
     sl.width = w;
   }
@@ -499,20 +550,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     int rc = drain(L.slot[j % kSlots]);
     if (rc) return rc;
   }
-  int status = 0;
-  if (!t.check.empty()) {
-    auto* hs = static_cast<int*>(L.hstatus.p);
-    for (int si = 0; si < nslots; ++si) {
-      Slot& sl = L.slot[si];
-      HIPCHK(hipMemcpyAsync(hs + si, static_cast<uint8_t*>(sl.meta.p) + ML.status_off,
-                            sizeof(int), hipMemcpyDeviceToHost, sl.stream));
-    }
-    for (int si = 0; si < nslots; ++si) {
-      HIPCHK(hipStreamSynchronize(L.slot[si].stream));
-      status |= hs[si];
-    }
-  }
-  return status ? RS_E_CORRUPT : RS_OK;
+  return corrupt ? RS_E_CORRUPT : RS_OK;
 }
 
 // Reconstruct's argument checks (upstream checkShards(shards, true)).
@@ -551,7 +589,7 @@ int reconstruct_host(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* 
   auto t = ctx->cache.get(k, m, present, verify);
   if (!t) return RS_E_SINGULAR;
   if (t->groups.empty()) return RS_OK;
-  rc = run_host(ctx, t, S, [&](int i) { return shards[i]; }, [&](int i) { return shards[i]; });
+  rc = run_host1(ctx, t, S, [&](int i) { return shards[i]; }, [&](int i) { return shards[i]; });
   if (rc == RS_OK || rc == RS_E_CORRUPT)
     for (int i : t->missing) lens[i] = S;
   return rc;
@@ -651,7 +689,7 @@ int rs_encode(rs_ctx* ctx, int k, int m, size_t S, const uint8_t* const* data,
   for (int i = 0; i < k + m; ++i) present[i] = i < k;
   auto t = ctx->cache.get(k, m, present, false);
   if (!t) return RS_E_SINGULAR;
-  return run_host(ctx, t, S, [&](int i) { return data[i]; },
+  return run_host1(ctx, t, S, [&](int i) { return data[i]; },
                   [&](int i) { return parity[i - k]; });
 }
 
@@ -680,7 +718,7 @@ int rs_codec_encode(rs_ctx* ctx, int k, int m, const uint8_t* data, size_t len,
   for (int i = 0; i < n; ++i) present[i] = i < k;
   auto t = ctx->cache.get(k, m, present, false);
   if (!t) return RS_E_SINGULAR;
-  return run_host(ctx, t, S, [&](int i) { return shards_out + S * i; },
+  return run_host1(ctx, t, S, [&](int i) { return shards_out + S * i; },
                   [&](int i) { return shards_out + S * i; });
 }
 
@@ -704,8 +742,8 @@ int rs_verify(rs_ctx* ctx, int k, int m, const uint8_t* const* shards, const siz
   for (int i = 0; i < n; ++i) present[i] = 1;
   auto t = ctx->cache.get(k, m, present, true);
   if (!t) return RS_E_SINGULAR;
-  rc = run_host(ctx, t, S, [&](int i) { return shards[i]; },
-                [&](int) { return static_cast<uint8_t*>(nullptr); });
+  rc = run_host1(ctx, t, S, [&](int i) { return shards[i]; },
+                 [&](int) { return static_cast<uint8_t*>(nullptr); });
   if (rc == RS_OK || rc == RS_E_CORRUPT) {
     *ok = rc == RS_OK;
     return RS_OK;
@@ -733,6 +771,113 @@ int rs_codec_decode(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* l
   }
   ctx->pool.run(segs);
   return RS_OK;
+}
+
+// ---- batched host-memory calls ---------------------------------------------------------
+
+namespace {
+
+// Stripes grouped by (S, presence): each group shares one table set and one pipeline.
+struct BatchGroups {
+  std::map<std::string, std::vector<int>> by_key;
+  void add(size_t S, const uint8_t* present, int n, int b) {
+    std::string key(reinterpret_cast<const char*>(&S), sizeof S);
+    key.append(reinterpret_cast<const char*>(present), n);
+    by_key[key].push_back(b);
+  }
+  static size_t shard_size(const std::string& key) {
+    size_t S;
+    std::memcpy(&S, key.data(), sizeof S);
+    return S;
+  }
+};
+
+int first_error(const int* status, int batch) {
+  for (int b = 0; b < batch; ++b)
+    if (status[b]) return status[b];
+  return RS_OK;
+}
+
+}  // namespace
+
+int rs_encode_batch(rs_ctx* ctx, int k, int m, int batch, const size_t* sizes,
+                    const uint8_t* const* data, uint8_t* const* parity, int* status) {
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!ctx || batch < 0 || (batch && (!sizes || !data || !parity || !status))) return RS_E_ARG;
+  const int n = k + m;
+  uint8_t present[256];
+  for (int i = 0; i < n; ++i) present[i] = i < k;
+  BatchGroups groups;
+  for (int b = 0; b < batch; ++b) {
+    status[b] = sizes[b] ? RS_OK : RS_E_NO_DATA;  // upstream Encode: ErrShardNoData
+    if (sizes[b]) groups.add(sizes[b], present, n, b);
+  }
+  auto t = ctx->cache.get(k, m, present, false);
+  if (!t) return RS_E_SINGULAR;
+  for (auto& kv : groups.by_key) {
+    const std::vector<int>& ids = kv.second;
+    const size_t S = BatchGroups::shard_size(kv.first);
+    rc = run_host(ctx, t, S, static_cast<int>(ids.size()),
+                  [&](int b, int i) { return data[static_cast<size_t>(ids[b]) * k + i]; },
+                  [&](int b, int i) { return parity[static_cast<size_t>(ids[b]) * m + i - k]; });
+    if (rc) return rc;
+  }
+  return first_error(status, batch);
+}
+
+int rs_reconstruct_batch(rs_ctx* ctx, int k, int m, int batch, uint8_t* const* shards,
+                         size_t* lens, int verify, int* status) {
+  int rc = check_profile(k, m);
+  if (rc) return rc;
+  if (!ctx || batch < 0 || (batch && (!shards || !lens || !status))) return RS_E_ARG;
+  const int n = k + m;
+  BatchGroups groups;
+  uint8_t present[256];
+  for (int b = 0; b < batch; ++b) {
+    uint8_t* const* sh = shards + static_cast<size_t>(b) * n;
+    const size_t* ln = lens + static_cast<size_t>(b) * n;
+    size_t S = 0;
+    int np = 0;
+    status[b] = check_lens(n, ln, true, &S, &np);
+    if (status[b]) continue;
+    if (np < k) {
+      status[b] = RS_E_TOO_FEW_SHARDS;
+      continue;
+    }
+    if (np == n && !verify) continue;
+    bool ok = true;
+    for (int i = 0; i < n; ++i) {
+      ok &= sh[i] != nullptr;
+      present[i] = ln[i] != 0;
+    }
+    if (!ok) {
+      status[b] = RS_E_ARG;
+      continue;
+    }
+    groups.add(S, present, n, b);
+  }
+  std::vector<int> flags;
+  for (auto& kv : groups.by_key) {
+    const std::vector<int>& ids = kv.second;
+    const size_t S = BatchGroups::shard_size(kv.first);
+    const uint8_t* pres = reinterpret_cast<const uint8_t*>(kv.first.data() + sizeof(size_t));
+    auto t = ctx->cache.get(k, m, pres, verify != 0);
+    if (!t) return RS_E_SINGULAR;
+    if (!t->groups.empty()) {
+      flags.assign(ids.size(), 0);
+      rc = run_host(ctx, t, S, static_cast<int>(ids.size()),
+                    [&](int b, int i) { return shards[static_cast<size_t>(ids[b]) * n + i]; },
+                    [&](int b, int i) { return shards[static_cast<size_t>(ids[b]) * n + i]; },
+                    flags.data());
+      if (rc != RS_OK && rc != RS_E_CORRUPT) return rc;
+      for (size_t j = 0; j < ids.size(); ++j)
+        if (flags[j]) status[ids[j]] = RS_E_CORRUPT;
+    }
+    for (int b : ids)
+      for (int i : t->missing) lens[static_cast<size_t>(b) * n + i] = S;
+  }
+  return first_error(status, batch);
 }
 
 // ---- device-resident ----------------------------------------------------------------

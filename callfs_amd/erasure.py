@@ -23,7 +23,7 @@ from __future__ import annotations
 import ctypes
 import hashlib
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -266,6 +266,70 @@ def verify(shards: List, k: int, m: int, context: Optional[N.Context] = None) ->
     if rc != N.RS_OK:
         raise _wrapped(rc, "verify")
     return bool(ok.value)
+
+
+# ---- batched host calls (many independent stripes per native call) ----------------
+
+def encode_batch(stripes: Sequence[Sequence], k: int, m: int,
+                 context: Optional[N.Context] = None) -> Tuple[List[List[bytearray]], List[int]]:
+    """rs_encode_batch: stripes[b] holds the k data shards of stripe b (equal length
+    within a stripe; stripes may differ). Returns (parity[b] = m fresh shards, status[b])
+    with status[b] one of RS_OK / RS_E_NO_DATA (empty shards)."""
+    ctx = context or N.default_context()
+    B = len(stripes)
+    sizes = (ctypes.c_size_t * max(B, 1))()
+    parity = []
+    for b, st in enumerate(stripes):
+        if len(st) != k:
+            raise ErrTooFewShards()
+        S = len(st[0])
+        if any(len(s) != S for s in st):
+            raise ErrShardSize()
+        sizes[b] = S
+        parity.append([bytearray(S) for _ in range(m)])
+    data = _shard_ptrs([s for st in stripes for s in st] or [None])
+    par = _shard_ptrs([p for ps in parity for p in ps] or [None])
+    status = (ctypes.c_int * max(B, 1))()
+    rc = N.lib.rs_encode_batch(ctx.handle, k, m, B, sizes, data, par, status)
+    if rc not in (N.RS_OK, N.RS_E_NO_DATA):
+        N.check(rc, "rs_encode_batch")
+    return parity, list(status)[:B]
+
+
+def reconstruct_batch(stripes: List[List], k: int, m: int, verify: bool = True,
+                      context: Optional[N.Context] = None) -> List[int]:
+    """rs_reconstruct_batch: stripes[b] is an n-list of shards (None / empty = missing),
+    reconstructed in place like reconstruct(); with verify the present parity beyond the
+    first k is re-checked per stripe. Returns status[b] (RS_OK, RS_E_CORRUPT,
+    RS_E_TOO_FEW_SHARDS, RS_E_SHARD_SIZE, RS_E_NO_DATA, ...)."""
+    ctx = context or N.default_context()
+    n = k + m
+    B = len(stripes)
+    flat, lens = [], (ctypes.c_size_t * max(B * n, 1))()
+    for b, st in enumerate(stripes):
+        if len(st) != n:
+            raise ErrTooFewShards()
+        ln = [0 if s is None else len(s) for s in st]
+        S = next((x for x in ln if x), 0)
+        for i in range(n):
+            lens[b * n + i] = ln[i]
+            if ln[i] == 0 and S:
+                st[i] = bytearray(S)  # upstream Reconstruct allocates missing shards
+        flat += st
+    status = (ctypes.c_int * max(B, 1))()
+    rc = N.lib.rs_reconstruct_batch(ctx.handle, k, m, B, _shard_ptrs(flat or [None]), lens,
+                                    int(verify), status)
+    if rc < 0 and rc not in (N.RS_E_CORRUPT, N.RS_E_TOO_FEW_SHARDS, N.RS_E_SHARD_SIZE,
+                             N.RS_E_NO_DATA):
+        if not (rc == N.RS_E_ARG and any(s == N.RS_E_ARG for s in list(status)[:B])):
+            N.check(rc, "rs_reconstruct_batch")
+    out = list(status)[:B]
+    for b, st in enumerate(stripes):  # stripes that failed keep their missing entries
+        if out[b] not in (N.RS_OK, N.RS_E_CORRUPT):
+            for i in range(n):
+                if lens[b * n + i] == 0:
+                    st[i] = None
+    return out
 
 
 # ---- host-side matrices (no device needed) ------------------------------------------

@@ -100,6 +100,27 @@ int rs_reconstruct(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* le
 int rs_verify(rs_ctx* ctx, int k, int m, const uint8_t* const* shards, const size_t* lens,
               int* ok);
 
+/* ---- Batched, host memory (many independent stripes per call) ----------------------
+ * Not in the reference API: for callers holding many objects at once (repair of every
+ * object that lost one shard, bulk re-encode, a server batching small uploads). Stripes
+ * are grouped by (S, presence) and each group runs one pipeline in which small stripes
+ * are packed many per H2D / launch / D2H, so a batch of 4 KiB objects costs a few round
+ * trips instead of one per object.
+ * rs_encode_batch: stripe b has sizes[b]-byte shards, data[b*k + i] / parity[b*m + j]
+ *   (= rs_encode per stripe, codec.go:36). sizes[b] == 0 -> status[b] = RS_E_NO_DATA.
+ * rs_reconstruct_batch: shards[b*n + i] / lens[b*n + i] with rs_reconstruct's contract
+ *   per stripe (codec.go:55); verify != 0 also re-checks the present parity beyond the
+ *   first k (codec.go:59) -> status[b] = RS_E_CORRUPT for that stripe alone.
+ * status[b] receives each stripe's code (RS_OK, RS_E_NO_DATA, RS_E_SHARD_SIZE,
+ * RS_E_TOO_FEW_SHARDS, RS_E_ARG, RS_E_CORRUPT). Returns RS_OK when every stripe is OK,
+ * else the first nonzero status in stripe order; a call-level error (RS_E_ARG,
+ * RS_E_INVALID_PROFILE, RS_E_HIP, RS_E_NOMEM) is returned directly with status[]
+ * unspecified. */
+int rs_encode_batch(rs_ctx* ctx, int k, int m, int batch, const size_t* sizes,
+                    const uint8_t* const* data, uint8_t* const* parity, int* status);
+int rs_reconstruct_batch(rs_ctx* ctx, int k, int m, int batch, uint8_t* const* shards,
+                         size_t* lens, int verify, int* status);
+
 /* ---- device-resident plans (batched stripes, graph-capturable launches) -------------
  * A plan fixes (k, m, S, batch, presence mask) and the device pointers of every
  * stripe's n shards: shards[b*n + i] is shard i of stripe b (device memory, S bytes).

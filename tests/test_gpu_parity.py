@@ -454,3 +454,98 @@ def test_one_gib_object_roundtrip(native_lib):
     dec.launch()
     assert not dec.corrupt()
     assert torch.equal(sb.buf[:, :, :S], ref)
+
+
+# ---- batched host calls (rs_encode_batch / rs_reconstruct_batch) --------------------
+
+@pytest.mark.parametrize("k,m", [(10, 4), (16, 4), (3, 2)])
+def test_encode_batch_mixed_sizes_match_oracle(native_lib, k, m):
+    """Many stripes per call, several shard sizes (grouped), one empty stripe."""
+    from callfs_amd import erasure as E
+    from callfs_amd._native import RS_E_NO_DATA, RS_OK
+    sizes = [256, 1, 4096, 333, 256, 65536, 0, 4096, 70001] * 7
+    stripes = [[rnd(1000 * b + i, S) for i in range(k)] for b, S in enumerate(sizes)]
+    parity, status = E.encode_batch(stripes, k, m)
+    for b, S in enumerate(sizes):
+        if S == 0:
+            assert status[b] == RS_E_NO_DATA
+            continue
+        assert status[b] == RS_OK
+        want = cref.encode([np.frombuffer(s, np.uint8) for s in stripes[b]], k, m)
+        for j in range(m):
+            assert bytes(parity[b][j]) == bytes(want[j]), (b, j)
+
+
+@pytest.mark.parametrize("k,m,S,B", [(4, 2, 1 << 20, 5),   # 2 stripes per chunk, per-shard DMA
+                                     (10, 4, 3 << 20, 3),  # one stripe over several column chunks
+                                     (16, 4, 256, 3000)])  # thousands of stripes per chunk
+def test_encode_batch_chunk_shapes(native_lib, k, m, S, B):
+    from callfs_amd import erasure as E
+    rng = np.random.default_rng(S + B)
+    stripes = [[rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] for _ in range(B)]
+    parity, status = E.encode_batch(stripes, k, m)
+    assert status == [0] * B
+    for b in sorted({0, B // 2, B - 1}):
+        want = cref.encode(stripes[b], k, m)
+        for j in range(m):
+            assert bytes(parity[b][j]) == bytes(want[j]), (b, j)
+
+
+def test_reconstruct_batch_mixed_patterns_and_errors(native_lib):
+    """Per-stripe erasures, a corrupt stripe, too-few and size-mismatch stripes."""
+    from callfs_amd import erasure as E
+    from callfs_amd._native import (RS_E_CORRUPT, RS_E_SHARD_SIZE, RS_E_TOO_FEW_SHARDS,
+                                    RS_OK)
+    k, m = 10, 4
+    n = k + m
+    patterns = [(), (0,), (0, 1, 2, 3), (0, 3, 7, 12), (10, 11, 12, 13), (5, 13)]
+    originals, stripes, expect = [], [], []
+    for b in range(48):
+        S = (1 << 12) if b % 3 else 100_003
+        data = [np.frombuffer(rnd(7 * b + i, S), np.uint8) for i in range(k)]
+        full = data + cref.encode(data, k, m)
+        originals.append(full)
+        st = [bytearray(x.tobytes()) for x in full]
+        for i in patterns[b % len(patterns)]:
+            st[i] = None
+        stripes.append(st)
+        expect.append(RS_OK)
+    # stripe 7: flip a byte of parity 13, present beyond the first k -> corrupt
+    stripes[7] = [bytearray(x.tobytes()) for x in originals[7]]
+    stripes[7][0] = None
+    stripes[7][13][5] ^= 1
+    expect[7] = RS_E_CORRUPT
+    # stripe 8: five erasures
+    for i in range(5):
+        stripes[8][i] = None
+    expect[8] = RS_E_TOO_FEW_SHARDS
+    # stripe 9: one short shard
+    stripes[9] = [bytearray(x.tobytes()) for x in originals[9]]
+    stripes[9][4] = stripes[9][4][:-1]
+    expect[9] = RS_E_SHARD_SIZE
+    status = E.reconstruct_batch(stripes, k, m, verify=True)
+    assert status == expect
+    for b in range(48):
+        if expect[b] != RS_OK:
+            continue
+        for i in range(n):
+            assert bytes(stripes[b][i]) == originals[b][i].tobytes(), (b, i)
+    assert stripes[8][0] is None  # failed stripes keep their missing entries
+
+
+def test_reconstruct_batch_matches_single_calls(native_lib):
+    """Batched results equal the per-object rs_reconstruct results (RS(16,4), 4 KiB)."""
+    from callfs_amd import erasure as E
+    k, m = 16, 4
+    stripes, singles = [], []
+    for b in range(500):
+        data = [np.frombuffer(rnd(31 * b + i, 256), np.uint8) for i in range(k)]
+        full = [bytearray(x.tobytes()) for x in data + cref.encode(data, k, m)]
+        for i in (b % 20, (b * 7 + 3) % 20):
+            full[i] = None
+        stripes.append(full)
+        singles.append(list(full))
+    assert E.reconstruct_batch(stripes, k, m, verify=False) == [0] * 500
+    for b in range(0, 500, 37):
+        E.reconstruct(singles[b], k, m)
+        assert [bytes(x) for x in stripes[b]] == [bytes(x) for x in singles[b]]

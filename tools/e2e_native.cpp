@@ -7,6 +7,8 @@
 // run:   tools/e2e_native k m object_bytes threads seconds [erase,list]
 // CALLFS_E2E_ENCODER=1: encode through rs_encode (Go-side Split aliasing the object,
 // parity only, as INTEGRATION.md's shim does) instead of rs_codec_encode.
+// CALLFS_E2E_BATCH=N: each call handles N objects through rs_encode_batch /
+// rs_reconstruct_batch (verify on) plus the per-object join copy.
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -39,6 +41,7 @@ int main(int argc, char** argv) {
     }
   }
   const bool encoder_api = std::getenv("CALLFS_E2E_ENCODER") != nullptr;
+  const int nb = std::getenv("CALLFS_E2E_BATCH") ? std::atoi(std::getenv("CALLFS_E2E_BATCH")) : 0;
   rs_ctx* ctx = nullptr;
   if (rs_init(&ctx, 0) != RS_OK) {
     std::fprintf(stderr, "rs_init failed\n");
@@ -73,9 +76,44 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> enc2(n * S);
         std::vector<uint8_t*> ptrs(n);
         std::vector<size_t> lens(n);
+        // batch mode: every object shares the same input bytes, outputs are per object
+        const int B = nb > 0 ? nb : 1;
+        std::vector<uint8_t> bout(nb > 0 ? static_cast<size_t>(B) * n * S : 0);
+        std::vector<const uint8_t*> bdata(nb > 0 ? static_cast<size_t>(B) * k : 0);
+        std::vector<uint8_t*> bpar(nb > 0 ? static_cast<size_t>(B) * m : 0);
+        std::vector<uint8_t*> bsh(nb > 0 ? static_cast<size_t>(B) * n : 0);
+        std::vector<size_t> bsz(B, S), blens(nb > 0 ? static_cast<size_t>(B) * n : 0);
+        std::vector<int> bst(B);
+        std::vector<uint8_t> bjoin(nb > 0 ? L : 0);
         while (!stop.load(std::memory_order_relaxed)) {
           int rc;
-          if (encode && encoder_api) {
+          if (nb > 0 && encode) {
+            for (int b = 0; b < B; ++b) {
+              for (int i = 0; i < k; ++i) bdata[static_cast<size_t>(b) * k + i] = me.enc.data() + S * i;
+              for (int j = 0; j < m; ++j)
+                bpar[static_cast<size_t>(b) * m + j] = bout.data() + (static_cast<size_t>(b) * n + k + j) * S;
+            }
+            rc = rs_encode_batch(ctx, k, m, B, bsz.data(), bdata.data(), bpar.data(), bst.data());
+          } else if (nb > 0) {
+            for (int b = 0; b < B; ++b)
+              for (int i = 0; i < n; ++i) {
+                bool gone = false;
+                for (int e : erase) gone |= e == i;
+                const size_t x = static_cast<size_t>(b) * n + i;
+                bsh[x] = gone ? bout.data() + x * S : me.sh[i].data();
+                blens[x] = gone ? 0 : S;
+              }
+            rc = rs_reconstruct_batch(ctx, k, m, B, bsh.data(), blens.data(), 1, bst.data());
+            for (int b = 0; b < B && rc == RS_OK; ++b) {  // join + trim per object
+              size_t left = L;
+              for (int i = 0; i < k && left; ++i) {
+                const size_t c = std::min(S, left);
+                std::memcpy(bjoin.data() + S * i, bsh[static_cast<size_t>(b) * n + i], c);
+                left -= c;
+              }
+              if (b == 0) me.out = bjoin;
+            }
+          } else if (encode && encoder_api) {
             // Split as upstream: full data shards alias src, the tail shard is a
             // zero-padded copy, parity lands in fresh buffers
             const size_t full = L / S;
@@ -107,7 +145,7 @@ int main(int argc, char** argv) {
                                  static_cast<int64_t>(L));
           }
           if (rc != RS_OK) me.err = rc;
-          ++me.ops;
+          me.ops += B;
         }
       });
     }
@@ -125,9 +163,9 @@ int main(int argc, char** argv) {
   int bad = 0;
   for (auto& x : th) bad |= x.err || x.out != x.src;
   std::printf("{\"api\": \"%s\", \"k\": %d, \"m\": %d, \"object_bytes\": %zu, \"threads\": %d, "
-              "\"erase_count\": %zu, \"encode_gib_s\": %.3f, \"decode_gib_s\": %.3f, "
+              "\"batch\": %d, \"erase_count\": %zu, \"encode_gib_s\": %.3f, \"decode_gib_s\": %.3f, "
               "\"encode_calls\": %ld, \"decode_calls\": %ld, \"ok\": %s}\n",
-              encoder_api ? "native-encoder" : "native", k, m, L, T, erase.size(), e.first, d.first, e.second, d.second, bad ? "false" : "true");
+              nb > 0 ? "native-batch" : encoder_api ? "native-encoder" : "native", k, m, L, T, nb > 0 ? nb : 1, erase.size(), e.first, d.first, e.second, d.second, bad ? "false" : "true");
   rs_shutdown(ctx);
   return bad ? 1 : 0;
 }
