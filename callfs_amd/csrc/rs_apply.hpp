@@ -363,6 +363,10 @@ void rs_apply_lds(ApplyArgs a) {
   constexpr int W = LdsAcc<RT>::W;
   using AccT = typename LdsAcc<RT>::T;
   const int K = a.K;
+  // RT = 16 serves every R in 9..16 (rows >= R are computed and dropped): an RT of
+  // 9..12 would let the compiler narrow the table reads to ds_read_b96, which ran
+  // RS(10,12) at 35 % of HBM against 59 % for the b128 reads of RS(10,16).
+  const int R = RT == 16 ? a.R : RT;
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.ltabs);
     uint4* dst = reinterpret_cast<uint4*>(smem);
@@ -376,7 +380,7 @@ void rs_apply_lds(ApplyArgs a) {
     const uint64_t v0 = static_cast<uint64_t>(t - stripe * tps) * BS + threadIdx.x;
     if (v0 >= a.nvec) continue;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
-    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * RT;
+    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
     auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
 
     AccT acc[4][4];
@@ -398,6 +402,7 @@ void rs_apply_lds(ApplyArgs a) {
     bool bad = false;
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
+      if (r >= R) continue;  // wave-uniform
       const uint4 o = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
                                  lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
       uint4* dst = reinterpret_cast<uint4*>(out[r]) + v0;

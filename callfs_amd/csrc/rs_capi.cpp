@@ -390,10 +390,8 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
                   size_t S, int batch, InF host_in, OutF host_out, int* stripe_status);
 
 template <class InF, class OutF>
-int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, int batch,
-             InF host_in, OutF host_out, int* stripe_status = nullptr) {
-  if (ctx->devs.empty()) return RS_E_HIP;
-  Device* dev = ctx->devs[ctx->rr.fetch_add(1) % ctx->devs.size()].get();
+int run_on(rs_ctx* ctx, Device* dev, const std::shared_ptr<const Tables>& tp, size_t S,
+           int batch, InF host_in, OutF host_out, int* stripe_status) {
   LaneGuard lg{ctx, dev, ctx->acquire(dev)};
   if (!lg.lane) return RS_E_HIP;
   const int rc =
@@ -406,6 +404,58 @@ int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, int
     }
   }
   return rc;
+}
+
+// Ways to split one large object's columns over (device, lane) pairs: every output
+// byte depends only on the same column of the inputs, so column ranges are independent
+// (the in-process form of bench.py's column_slices). Objects of at least
+// CALLFS_RS_SPLIT_MIN_BYTES over all n shards (default 256 MiB) are split
+// CALLFS_RS_SPLIT_WAYS ways (default: one per device), each way on its own lane, so a
+// multi-GPU host moves one object over every GPU's PCIe link at once.
+int split_ways(const rs_ctx* ctx, size_t S, int n, int batch) {
+  if (batch != 1) return 1;
+  const char* e = std::getenv("CALLFS_RS_SPLIT_MIN_BYTES");
+  const unsigned long long min_bytes = e ? std::strtoull(e, nullptr, 0) : (256ull << 20);
+  if (static_cast<unsigned long long>(S) * n < min_bytes) return 1;
+  const char* w = std::getenv("CALLFS_RS_SPLIT_WAYS");
+  int ways = w ? std::atoi(w) : static_cast<int>(ctx->devs.size());
+  ways = std::max(1, std::min(ways, static_cast<int>(ctx->devs.size()) * kMaxLanesPerDevice));
+  // at least 4 MiB of columns per way
+  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(ways, S >> 22)));
+}
+
+template <class InF, class OutF>
+int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, int batch,
+             InF host_in, OutF host_out, int* stripe_status = nullptr) {
+  if (ctx->devs.empty()) return RS_E_HIP;
+  const size_t nd = ctx->devs.size();
+  const unsigned base = ctx->rr.fetch_add(1);
+  const int ways = split_ways(ctx, S, tp->k + tp->m, batch);
+  if (ways == 1)
+    return run_on(ctx, ctx->devs[base % nd].get(), tp, S, batch, host_in, host_out,
+                  stripe_status);
+  // column parts [c[p], c[p+1]), 4 KiB aligned
+  std::vector<size_t> c(ways + 1, 0);
+  for (int p = 1; p < ways; ++p) c[p] = std::min(S, round_up(S / ways * p, 4096));
+  c[ways] = S;
+  std::vector<int> rc(ways, RS_OK), flag(ways, 0);
+  std::vector<std::thread> th;
+  for (int p = 0; p < ways; ++p)
+    th.emplace_back([&, p] {
+      const size_t c0 = c[p];
+      if (c[p + 1] <= c0) return;
+      rc[p] = run_on(ctx, ctx->devs[(base + p) % nd].get(), tp, c[p + 1] - c0, 1,
+                     [&](int b, int i) { return host_in(b, i) + c0; },
+                     [&](int b, int i) { return host_out(b, i) + c0; }, &flag[p]);
+    });
+  for (auto& t : th) t.join();
+  int out = RS_OK;
+  for (int p = 0; p < ways; ++p) {
+    if (rc[p] != RS_OK && rc[p] != RS_E_CORRUPT) return rc[p];
+    if (rc[p] == RS_E_CORRUPT) out = RS_E_CORRUPT;
+  }
+  if (out == RS_E_CORRUPT && stripe_status) stripe_status[0] = 1;
+  return out;
 }
 
 // Single-stripe form used by the per-object entry points.

@@ -47,7 +47,9 @@ constexpr auto byte_table(std::integer_sequence<int, Rs...>) {
 }
 
 const auto kVec = vec_table(std::make_integer_sequence<int, kPermMaxRows>{});
-const auto kLds = lds_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
+// R 1..8 exact; R 9..16 share the 16-row instance (rs_apply_lds: b128 table reads).
+const auto kLds = lds_table(std::make_integer_sequence<int, kPermMaxRows>{});
+const VecFn kLdsWide = &dev::rs_apply_lds<kMaxRowsPerLaunch, LdsPolicy>;
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
 }  // namespace
@@ -64,10 +66,11 @@ hipError_t launch_apply(ApplyArgs a, bool aligned, hipStream_t stream) {
       if (a.R >= kLdsMinRows || a.R > kPermMaxRows) {
         if (!a.ltabs) return hipErrorInvalidValue;
         const size_t lds = dev::lds_bytes(a.K, a.R);
-        VecFn fn = kLds[a.R - 1];
+        const int fi = a.R > kPermMaxRows ? kPermMaxRows : a.R - 1;
+        VecFn fn = a.R > kPermMaxRows ? kLdsWide : kLds[fi];
         if (lds > (64u << 10)) {  // wide groups with many shards: opt in once per kernel
-          static std::once_flag once[kMaxRowsPerLaunch];
-          std::call_once(once[a.R - 1], [fn] {
+          static std::once_flag once[kPermMaxRows + 1];
+          std::call_once(once[fi], [fn] {
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
           });

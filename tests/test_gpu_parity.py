@@ -549,3 +549,30 @@ def test_reconstruct_batch_matches_single_calls(native_lib):
     for b in range(0, 500, 37):
         E.reconstruct(singles[b], k, m)
         assert [bytes(x) for x in stripes[b]] == [bytes(x) for x in singles[b]]
+
+
+# ---- one object split over lanes / devices (CALLFS_RS_SPLIT_*) ----------------------
+
+@pytest.mark.parametrize("ways", [2, 3, 5])
+def test_split_object_roundtrip_and_corruption(codec, monkeypatch, ways):
+    """Column split of a single object over `ways` lanes: bytes equal the oracle, decode
+    restores the object, and a flipped parity byte in one part still reports corruption."""
+    from callfs_amd import ErasureProfile, ErrShardCorrupted
+    monkeypatch.setenv("CALLFS_RS_SPLIT_MIN_BYTES", str(1 << 20))
+    monkeypatch.setenv("CALLFS_RS_SPLIT_WAYS", str(ways))
+    k, m = 10, 4
+    L = 130_000_017  # S = 13,000,002: ragged, 4 KiB-aligned part boundaries inside
+    data = rnd(ways, L)
+    shards = codec.encode(data, ErasureProfile(k, m))
+    want = oracle_shards(data, k, m)
+    for i in range(k, k + m):
+        assert bytes(shards[i]) == want[i].tobytes(), i
+    got = [bytearray(s) for s in shards]
+    for i in (0, 3, 7, 12):
+        got[i] = None
+    assert codec.decode(got, ErasureProfile(k, m), L) == data
+    bad = [bytearray(s) for s in shards]
+    bad[1] = None
+    bad[13][len(bad[13]) - 5] ^= 0x40  # last part of the columns; parity 13 is checked
+    with pytest.raises(ErrShardCorrupted):
+        codec.decode(bad, ErasureProfile(k, m), L)

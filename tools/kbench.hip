@@ -7,7 +7,8 @@
 // an XOR-only kernel with the identical access pattern (K loads + R stores per 16-B
 // vector, no GF work) as the memory ceiling of this traffic shape, and hipMemcpy D2D.
 //
-// build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I callfs_amd/csrc tools/kbench.hip -o tools/kbench
+// build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I callfs_amd/csrc tools/kbench.hip \
+//          callfs_amd/csrc/rs_kernels.hip -o tools/kbench
 // run:   tools/kbench [k m shard_bytes stripes rounds iters]
 #include <hip/hip_runtime.h>
 
@@ -21,6 +22,7 @@
 
 #include "gf256.hpp"
 #include "rs_apply.hpp"
+#include "rs_kernels.hpp"
 
 using namespace callfs;
 
@@ -189,7 +191,11 @@ int main(int argc, char** argv) {
   using namespace dev;
   using Prod = Policy<4, 1, true, true, false, 512, 2, 0>;  // = rs_kernels.hip ProdPolicy
   std::vector<Variant> vs;
-  switch (m) {  // production kernel (runtime K) for this row count
+  // what the library runs for this (K, R): rs_kernels.hip launch_apply's dispatch
+  vs.push_back(Variant{"prod dispatch", [](const ApplyArgs& a, hipStream_t s) {
+                         CK(launch_apply(a, true, s));
+                       }});
+  switch (m) {  // v_perm kernel (runtime K) for this row count
     case 1: vs.push_back(make_variant<0, 1, Prod>("prod rtK nt")); break;
     case 2: vs.push_back(make_variant<0, 2, Prod>("prod rtK nt")); break;
     case 3: vs.push_back(make_variant<0, 3, Prod>("prod rtK nt")); break;
@@ -222,10 +228,10 @@ int main(int argc, char** argv) {
       vs.push_back(Variant{"lds bs512", [](const ApplyArgs& a, hipStream_t s) { launch_lds<6, L512>(a, s); }});
       break;
     case 12:
-      vs.push_back(Variant{"lds b128 (prod R 9..16)", [](const ApplyArgs& a, hipStream_t s) { launch_lds<12, L512w2>(a, s); }});
+      vs.push_back(Variant{"lds RT=12 (b96 reads, r01 prod)", [](const ApplyArgs& a, hipStream_t s) { launch_lds<12, L512w2>(a, s); }});
       break;
     case 16:
-      vs.push_back(Variant{"lds b128 (prod R 9..16)", [](const ApplyArgs& a, hipStream_t s) { launch_lds<16, L512w2>(a, s); }});
+      vs.push_back(Variant{"lds RT=16 direct", [](const ApplyArgs& a, hipStream_t s) { launch_lds<16, L512w2>(a, s); }});
       break;
   }
   if (rs10_4) vs.push_back(Variant{"read-only 10 streams (bytes: 10/14)", [](const ApplyArgs& a, hipStream_t s) {
