@@ -137,6 +137,9 @@ def load_traffic(path, cfg):
 def main(argv=None):
     args = parse_args(argv)
     rank, world, local = dist_env()
+    # one GPU per rank on a full node; ranks beyond the device count share devices
+    # (device_count() does not initialise HIP), which lets a 1-GPU box rehearse N > 1
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
