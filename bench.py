@@ -17,8 +17,9 @@ each rank encodes/decodes its own batch with no data-path collective ("weak"
 scaling). The only cross-rank traffic is the gloo barrier and the max-reduce of the
 timer.
 
-roofline: the encode kernel's algorithmic bytes per launch ((k+m)*S per stripe) over
-its average HIP-event duration on the launch stream, against 8.0 TB/s HBM3E.
+roofline: the encode kernel's (rs_apply_lds for k >= 4) algorithmic bytes per launch
+((k+m)*S per stripe) over its average HIP-event duration on the launch stream, against
+8.0 TB/s HBM3E.
 cpu_baseline: rank 0 at N=1 only — the C port of the reference CPU algorithm
 (oracle/rs_oracle.c: upstream GFNI/AVX2 strategy, byte-range threads) on a bounded
 sample of the same stripes; the same leg checks the GPU parity of those stripes
@@ -243,7 +244,7 @@ def main(argv=None):
         "decode_ms": round(dec_ms, 4),
         "roofline": {
             "bound": "hbm",
-            "kernel": "rs_apply_vec (encode plan)",
+            "kernel": ("rs_apply_lds" if k >= 4 else "rs_apply_vec") + " (encode plan)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

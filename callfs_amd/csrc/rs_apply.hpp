@@ -289,20 +289,43 @@ struct LdsAcc {
       (RT > 8), u32x4_acc, typename std::conditional<(RT > 4), uint64_t, uint32_t>::type>::type;
 };
 
+template <class T>
+using lds_ptr = const __attribute__((address_space(3))) T*;
+
+// One table entry at an absolute 32-bit LDS address (no base add per lookup).
 template <int RT>
-__device__ __forceinline__ typename LdsAcc<RT>::T lds_lookup(const uint8_t* smem, uint32_t addr) {
+__device__ __forceinline__ typename LdsAcc<RT>::T lds_lookup(uint32_t addr) {
   using T = typename LdsAcc<RT>::T;
   if constexpr (RT > 8) {
-    const uint4 q = *reinterpret_cast<const uint4*>(smem + addr);
+    const u32x4 q = *(lds_ptr<u32x4>)(static_cast<uintptr_t>(addr));
     return T{{q.x, q.y, q.z, q.w}};
   } else {
-    return *reinterpret_cast<const T*>(smem + addr);
+    return *(lds_ptr<T>)(static_cast<uintptr_t>(addr));
   }
 }
 
+// a ^ b ^ c with one v_bitop3 per dword.
+__device__ __forceinline__ uint32_t lds_x3(uint32_t a, uint32_t b, uint32_t c) {
+  return xor3(a, b, c);
+}
+__device__ __forceinline__ uint64_t lds_x3(uint64_t a, uint64_t b, uint64_t c) {
+  return (static_cast<uint64_t>(xor3(a >> 32, b >> 32, c >> 32)) << 32) |
+         xor3(static_cast<uint32_t>(a), static_cast<uint32_t>(b), static_cast<uint32_t>(c));
+}
+__device__ __forceinline__ u32x4_acc lds_x3(const u32x4_acc& a, const u32x4_acc& b,
+                                            const u32x4_acc& c) {
+  return u32x4_acc{{xor3(a.v[0], b.v[0], c.v[0]), xor3(a.v[1], b.v[1], c.v[1]),
+                    xor3(a.v[2], b.v[2], c.v[2]), xor3(a.v[3], b.v[3], c.v[3])}};
+}
+
+// base: absolute LDS address of input shard i's tables (256-B aligned).
+// All 8 lookups of a data dword are issued before any is consumed; for 16-byte entries
+// a sched_group_barrier keeps them together (the default schedule reused one register
+// quad and waited after every pair: 2 reads in flight instead of 8).
 template <int RT>
 __device__ __forceinline__ void lds_mac(typename LdsAcc<RT>::T (&acc)[4][4], const uint4& x,
-                                        const uint8_t* smem, uint32_t base) {
+                                        uint32_t base) {
+  using T = typename LdsAcc<RT>::T;
   constexpr int W = LdsAcc<RT>::W;
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
@@ -317,13 +340,19 @@ __device__ __forceinline__ void lds_mac(typename LdsAcc<RT>::T (&acc)[4][4], con
       xh = xw & 0xf0f0f0f0u;
       base_hi = base + 256u;
     }
+    T lo[4], hi[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t sel = 0x07060500u | static_cast<uint32_t>(j);
-      const auto lo = lds_lookup<RT>(smem, __builtin_amdgcn_perm(base, xl, sel));
-      const auto hi = lds_lookup<RT>(smem, __builtin_amdgcn_perm(base_hi, xh, sel));
-      acc[w][j] = acc[w][j] ^ lo ^ hi;
+      lo[j] = lds_lookup<RT>(__builtin_amdgcn_perm(base, xl, sel));
+      hi[j] = lds_lookup<RT>(__builtin_amdgcn_perm(base_hi, xh, sel));
     }
+    if constexpr (W == 16) {
+      __builtin_amdgcn_sched_group_barrier(0x0100, 8, 0);  // the 8 DS reads
+      __builtin_amdgcn_sched_group_barrier(0x0002, 64, 0);  // then VALU
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[w][j] = lds_x3(acc[w][j], lo[j], hi[j]);
   }
 }
 
@@ -355,24 +384,31 @@ __device__ __forceinline__ typename LdsAcc<RT>::T lds_zero() {
   else return 0;
 }
 
+// Waves per SIMD the LDS kernel may be limited to: 16-byte entries keep 8 b128 reads
+// (32 VGPRs) in flight, which the register allocator only grants below 5 waves.
+template <int RT>
+constexpr int lds_max_waves() { return RT > 8 ? 4 : 8; }
+
 template <int RT, class P>
-__global__ __launch_bounds__(P::BS) __attribute__((amdgpu_waves_per_eu(P::WPE, 8)))
+__global__ __launch_bounds__(P::BS) __attribute__((amdgpu_waves_per_eu(P::WPE, lds_max_waves<RT>())))
 void rs_apply_lds(ApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int BS = P::BS;
   constexpr int W = LdsAcc<RT>::W;
   using AccT = typename LdsAcc<RT>::T;
   const int K = a.K;
-  // RT = 16 serves every R in 9..16 (rows >= R are computed and dropped): an RT of
-  // 9..12 would let the compiler narrow the table reads to ds_read_b96, which ran
-  // RS(10,12) at 35 % of HBM against 59 % for the b128 reads of RS(10,16).
-  const int R = RT == 16 ? a.R : RT;
+  // the launch passes R == RT; kept as a runtime stride so an RT instance can also
+  // serve fewer rows (rows >= R are computed and dropped)
+  const int R = a.R;
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.ltabs);
     uint4* dst = reinterpret_cast<uint4*>(smem);
     for (int j = threadIdx.x; j < K * 2 * W; j += BS) dst[j] = src[j];
   }
   __syncthreads();
+  // absolute LDS address of the tables (0 unless static LDS is ever added)
+  const uint32_t lds0 = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)smem));
   const uint32_t tps = static_cast<uint32_t>((a.nvec + BS - 1) / BS);
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
   for (uint32_t t = blockIdx.x; t < ntiles; t += ntiles) {
@@ -394,7 +430,7 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll 1
     for (int i = 0; i < K; ++i) {
       if (i + 2 < K) x2 = ld(i + 2);
-      lds_mac<RT>(acc, x0, smem, static_cast<uint32_t>(i) * 32u * W);
+      lds_mac<RT>(acc, x0, lds0 + static_cast<uint32_t>(i) * 32u * W);
       x0 = x1;
       x1 = x2;
     }

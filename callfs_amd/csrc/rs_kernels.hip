@@ -14,19 +14,24 @@ namespace {
 
 using dev::kBlock;
 
-// Production policy (tools/kbench.hip on MI355X, RS(10,4) 1 MiB shards x 256 stripes,
+// v_perm kernel policy (tools/kbench.hip on MI355X, RS(10,4) 1 MiB shards x 256 stripes,
 // DESIGN.md "Kernel tuning log"): runtime-K pair loop, non-temporal loads and stores,
 // 512-thread blocks, two input pairs in flight = 6118-6168 GB/s (76.5-77.1 % of
 // 8 TB/s) vs 5457 GB/s for the first compile-time-K / plain-load version and
-// 5957 GB/s for an XOR-only kernel with the same loads and stores.
+// 5957 GB/s for an XOR-only kernel with the same loads and stores. Used for k <= 3.
 using ProdPolicy = dev::Policy<4, 1, true, true, false, 512, 2, 0>;
 
-// Row groups of 5..16 use the LDS nibble-table kernel: its cost does not grow with the
-// row count (RS(10,8): 5,749 vs 4,887 GB/s; RS(32,8): 4,783 vs 3,948; RS(12,6): 5,318
-// vs 5,118 — tools/kbench.hip), while for R <= 4 the v_perm kernel is faster.
+// The LDS nibble-table kernel takes every launch with k >= 4 inputs or R >= 5 rows. Its
+// cost per data byte barely grows with R, and with all 8 lookups of a dword in flight it
+// also beats the v_perm kernel at R <= 4 (tools/kbench.hip, rotated order, 5 rounds,
+// % of 8 TB/s): RS(10,4) 78.6 vs 73.0-75.7, RS(16,4) 77.4 vs 72.2-73.2, RS(20,4) 75.9
+// vs 70.2-71.2, RS(4,2) 78.6 vs 76.6, RS(10,8) 71-72 vs 62, RS(32,8) 69.7 vs 49.3.
+// With k <= 3 the per-block table prologue does not pay (RS(3,2): 73.3 vs 77.5-79.9),
+// so those launches keep the v_perm kernel. One instance per R.
 using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
 constexpr int kLdsMinRows = 5;
-constexpr int kPermMaxRows = 8;  // v_perm kernel instantiations (production uses <= 4)
+constexpr int kLdsMinK = 4;
+constexpr int kPermMaxRows = 8;  // v_perm kernel instantiations (production: k <= 3, R <= 4)
 
 using VecFn = void (*)(ApplyArgs);
 using ByteFn = void (*)(ApplyArgs, uint64_t);
@@ -47,9 +52,7 @@ constexpr auto byte_table(std::integer_sequence<int, Rs...>) {
 }
 
 const auto kVec = vec_table(std::make_integer_sequence<int, kPermMaxRows>{});
-// R 1..8 exact; R 9..16 share the 16-row instance (rs_apply_lds: b128 table reads).
-const auto kLds = lds_table(std::make_integer_sequence<int, kPermMaxRows>{});
-const VecFn kLdsWide = &dev::rs_apply_lds<kMaxRowsPerLaunch, LdsPolicy>;
+const auto kLds = lds_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
 }  // namespace
@@ -63,14 +66,13 @@ hipError_t launch_apply(ApplyArgs a, bool aligned, hipStream_t stream) {
     a.nvec = a.S / 16;
     tail0 = a.nvec * 16;
     if (a.nvec) {
-      if (a.R >= kLdsMinRows || a.R > kPermMaxRows) {
+      if (a.R >= kLdsMinRows || a.K >= kLdsMinK) {
         if (!a.ltabs) return hipErrorInvalidValue;
         const size_t lds = dev::lds_bytes(a.K, a.R);
-        const int fi = a.R > kPermMaxRows ? kPermMaxRows : a.R - 1;
-        VecFn fn = a.R > kPermMaxRows ? kLdsWide : kLds[fi];
+        VecFn fn = kLds[a.R - 1];
         if (lds > (64u << 10)) {  // wide groups with many shards: opt in once per kernel
-          static std::once_flag once[kPermMaxRows + 1];
-          std::call_once(once[fi], [fn] {
+          static std::once_flag once[kMaxRowsPerLaunch];
+          std::call_once(once[a.R - 1], [fn] {
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
           });

@@ -127,7 +127,7 @@ def test_golden_fixtures(codec):
 
 # R = m rows per launch group: 1..4 take the v_perm kernel, 5..8 the LDS kernel with
 # 8-byte nibble entries, 9..16 with 16-byte entries; m > 16 splits (20 = 16+4).
-PROFILES = [(1, 1), (2, 1), (3, 2), (4, 2), (5, 5), (6, 3), (8, 4), (10, 4), (12, 4),
+PROFILES = [(1, 1), (2, 1), (3, 2), (2, 3), (3, 4), (4, 2), (5, 5), (6, 3), (8, 4), (10, 4), (12, 4),
             (16, 4), (17, 3), (10, 6), (12, 7), (20, 10), (32, 8), (6, 9), (4, 13),
             (10, 12), (12, 16), (40, 20)]
 

@@ -227,12 +227,21 @@ int main(int argc, char** argv) {
     case 6:
       vs.push_back(Variant{"lds bs512", [](const ApplyArgs& a, hipStream_t s) { launch_lds<6, L512>(a, s); }});
       break;
-    case 12:
-      vs.push_back(Variant{"lds RT=12 (b96 reads, r01 prod)", [](const ApplyArgs& a, hipStream_t s) { launch_lds<12, L512w2>(a, s); }});
-      break;
+    case 9: vs.push_back(Variant{"lds RT=9", [](const ApplyArgs& a, hipStream_t s) { launch_lds<9, L512w2>(a, s); }}); break;
+    case 10: vs.push_back(Variant{"lds RT=10", [](const ApplyArgs& a, hipStream_t s) { launch_lds<10, L512w2>(a, s); }}); break;
+    case 11: vs.push_back(Variant{"lds RT=11", [](const ApplyArgs& a, hipStream_t s) { launch_lds<11, L512w2>(a, s); }}); break;
+    case 12: vs.push_back(Variant{"lds RT=12", [](const ApplyArgs& a, hipStream_t s) { launch_lds<12, L512w2>(a, s); }}); break;
+    case 13: vs.push_back(Variant{"lds RT=13", [](const ApplyArgs& a, hipStream_t s) { launch_lds<13, L512w2>(a, s); }}); break;
+    case 14: vs.push_back(Variant{"lds RT=14", [](const ApplyArgs& a, hipStream_t s) { launch_lds<14, L512w2>(a, s); }}); break;
+    case 15: vs.push_back(Variant{"lds RT=15", [](const ApplyArgs& a, hipStream_t s) { launch_lds<15, L512w2>(a, s); }}); break;
     case 16:
       vs.push_back(Variant{"lds RT=16 direct", [](const ApplyArgs& a, hipStream_t s) { launch_lds<16, L512w2>(a, s); }});
       break;
+  }
+  if (m <= 4) {  // LDS kernel with the production LDS policy, for the R <= 4 dispatch choice
+    static void (*const lds_r[4])(const ApplyArgs&, hipStream_t) = {
+        launch_lds<1, L512w2>, launch_lds<2, L512w2>, launch_lds<3, L512w2>, launch_lds<4, L512w2>};
+    vs.push_back(Variant{"lds prod-policy", [m](const ApplyArgs& a, hipStream_t s) { lds_r[m - 1](a, s); }});
   }
   if (rs10_4) vs.push_back(Variant{"read-only 10 streams (bytes: 10/14)", [](const ApplyArgs& a, hipStream_t s) {
                          const unsigned g = static_cast<unsigned>((a.nvec + 511) / 512 * a.batch);
@@ -272,8 +281,12 @@ int main(int argc, char** argv) {
   std::vector<std::vector<double>> ms(vs.size());
   std::vector<uint8_t> h1(m * pitch), h2(m * pitch);
   for (int rd = 0; rd < rounds; ++rd) {
-    for (size_t vi = 0; vi < vs.size(); ++vi) {
+    // rotate the order each round: the variant timed right after the D2D copy ran
+    // ~3 % slow when it always went first
+    for (size_t vj = 0; vj < vs.size(); ++vj) {
+      const size_t vi = (vj + rd) % vs.size();
       vs[vi].launch(a, s);  // warm
+      vs[vi].launch(a, s);
       CK(hipEventRecord(e0, s));
       for (int it = 0; it < iters; ++it) vs[vi].launch(a, s);
       CK(hipEventRecord(e1, s));

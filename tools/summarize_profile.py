@@ -8,7 +8,7 @@ import statistics
 import sys
 
 
-def main(src, dst, k=10, m=4, S=1 << 20, B=256, kernel="rs_apply_vec"):
+def main(src, dst, k=10, m=4, S=1 << 20, B=256, kernel="rs_apply_lds"):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     rows = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
@@ -38,6 +38,17 @@ def main(src, dst, k=10, m=4, S=1 << 20, B=256, kernel="rs_apply_vec"):
         "encode_bytes_per_launch": fetch_b + write_b,
         "algorithmic_bytes_per_launch": B * S * (k + m),
     }
+    trace = os.path.join(src, "kt", "kt_kernel_trace.csv")
+    if os.path.exists(trace):  # per-dispatch rows of the hot kernel
+        rows = list(csv.DictReader(open(trace)))
+        hot = [r for r in rows if kernel in r.get("Kernel_Name", "")]
+        if hot:
+            with open(os.path.join(dst, "kernel_trace_rs_apply.csv"), "w", newline="") as f:
+                w = csv.DictWriter(f, fieldnames=list(hot[0].keys()))
+                w.writeheader()
+                w.writerows(hot)
+            durs = sorted(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in hot)
+            out["kernel_trace"]["median_ns"] = durs[len(durs) // 2]
     json.dump(out, open(os.path.join(dst, "hbm_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
