@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void xor_stream(ApplyArgs a) {
 
 template <int R, class P>
 void launch_lds(const ApplyArgs& a, hipStream_t s) {
-  const unsigned g = static_cast<unsigned>((a.nvec + P::BS - 1) / P::BS * a.batch);
+  const unsigned g = dev::vec_grid<P>(a.nvec, a.batch);
   hipLaunchKernelGGL((dev::rs_apply_lds<R, P>), dim3(g), dim3(P::BS), dev::lds_bytes(a.K, R), s, a);
 }
 
@@ -129,12 +129,13 @@ int main(int argc, char** argv) {
   const int rounds = argc > 5 ? std::atoi(argv[5]) : 5;
   const int iters = argc > 6 ? std::atoi(argv[6]) : 10;
   const size_t palign = argc > 7 ? std::strtoull(argv[7], nullptr, 0) : 256;
+  const size_t ppad = argc > 8 ? std::strtoull(argv[8], nullptr, 0) : 0;  // extra bytes per shard
   if (m < 1 || m > 16 || k < 1 || k > 256) {
     std::fprintf(stderr, "need 1<=m<=16, 1<=k<=256\n");
     return 2;
   }
   const int n = k + m;
-  const size_t pitch = (S + palign - 1) / palign * palign;
+  const size_t pitch = (S + palign - 1) / palign * palign + ppad;
   const size_t total = pitch * n * B;
   uint8_t* buf;
   CK(hipMalloc(&buf, total));
@@ -158,9 +159,27 @@ int main(int argc, char** argv) {
   }
   std::vector<const uint8_t*> in(static_cast<size_t>(B) * k);
   std::vector<uint8_t*> out(static_cast<size_t>(B) * m);
+  // KB_IN / KB_OUT: comma lists of the stripe slots read / written (a decode pattern's
+  // shard placement); default slots 0..k-1 in, k..n-1 out
+  std::vector<int> islot(k), oslot(m);
+  for (int i = 0; i < k; ++i) islot[i] = i;
+  for (int r = 0; r < m; ++r) oslot[r] = k + r;
+  auto parse = [](const char* e, std::vector<int>& v) {
+    if (!e) return;
+    std::string str(e);
+    size_t p = 0;
+    for (int& x : v) {
+      x = std::atoi(str.c_str() + p);
+      p = str.find(',', p);
+      if (p == std::string::npos) break;
+      ++p;
+    }
+  };
+  parse(std::getenv("KB_IN"), islot);
+  parse(std::getenv("KB_OUT"), oslot);
   for (int b = 0; b < B; ++b) {
-    for (int i = 0; i < k; ++i) in[b * k + i] = buf + (static_cast<size_t>(b) * n + i) * pitch;
-    for (int r = 0; r < m; ++r) out[b * m + r] = buf + (static_cast<size_t>(b) * n + k + r) * pitch;
+    for (int i = 0; i < k; ++i) in[b * k + i] = buf + (static_cast<size_t>(b) * n + islot[i]) * pitch;
+    for (int r = 0; r < m; ++r) out[b * m + r] = buf + (static_cast<size_t>(b) * n + oslot[r]) * pitch;
   }
   void *d_in, *d_out, *d_tabs, *d_ltabs;
   int* d_status;
@@ -265,6 +284,26 @@ int main(int argc, char** argv) {
                          CK(hipMemcpyAsync(buf + half, buf, half, hipMemcpyDeviceToDevice, s));
                        }, false});
 
+  // KB_KEEP="a|b|...": keep only the variants whose name contains one of these (the
+  // first variant, the production dispatch, is always kept: it is the parity reference)
+  if (const char* keep = std::getenv("KB_KEEP")) {
+    std::vector<std::string> pats;
+    std::string ks(keep);
+    for (size_t p = 0; p <= ks.size();) {
+      size_t q = ks.find('|', p);
+      if (q == std::string::npos) q = ks.size();
+      if (q > p) pats.push_back(ks.substr(p, q - p));
+      p = q + 1;
+    }
+    std::vector<Variant> kept{vs[0]};
+    for (size_t i = 1; i < vs.size(); ++i)
+      for (auto& pt : pats)
+        if (vs[i].name.find(pt) != std::string::npos) {
+          kept.push_back(vs[i]);
+          break;
+        }
+    vs.swap(kept);
+  }
   hipStream_t s;
   CK(hipStreamCreate(&s));
   hipEvent_t e0, e1;
@@ -277,6 +316,10 @@ int main(int argc, char** argv) {
   for (int b = 0; b < B; ++b)
     CK(hipMemcpy(ref + static_cast<size_t>(b) * m * pitch, out[b * m], m * pitch, hipMemcpyDeviceToDevice));
 
+  // KB_VERIFY=mask: rows with these bits compare against the parity just written
+  // (upstream Verify) instead of storing; the status word must stay 0
+  const unsigned vmask = std::getenv("KB_VERIFY") ? std::strtoul(std::getenv("KB_VERIFY"), nullptr, 0) : 0;
+  a.verify_mask = vmask;
   const double bytes = static_cast<double>(B) * S * n;
   std::vector<std::vector<double>> ms(vs.size());
   std::vector<uint8_t> h1(m * pitch), h2(m * pitch);
@@ -310,8 +353,15 @@ int main(int argc, char** argv) {
       }
     }
   }
-  std::printf("RS(%d,%d) S=%zu pitch=%zu stripes=%d  working set %.2f GiB  rounds=%d iters=%d\n", k, m,
-              S, pitch, B, total / 1073741824.0, rounds, iters);
+  std::printf("RS(%d,%d) S=%zu pitch=%zu stripes=%d  working set %.2f GiB  rounds=%d iters=%d  in=%s out=%s\n",
+              k, m, S, pitch, B, total / 1073741824.0, rounds, iters,
+              std::getenv("KB_IN") ? std::getenv("KB_IN") : "0..k-1",
+              std::getenv("KB_OUT") ? std::getenv("KB_OUT") : "k..n-1");
+  if (vmask) {
+    int st = 0;
+    CK(hipMemcpy(&st, d_status, 4, hipMemcpyDeviceToHost));
+    std::printf("verify_mask=0x%x status=%d%s\n", vmask, st, st ? "  MISMATCH (verify flagged)" : "");
+  }
   std::printf("%-28s %10s %10s %10s %8s\n", "variant", "med_us", "min_us", "GB/s(med)", "%8TB/s");
   for (size_t vi = 0; vi < vs.size(); ++vi) {
     auto v = ms[vi];
@@ -320,6 +370,8 @@ int main(int argc, char** argv) {
     double frac = 1.0;
     if (vs[vi].name.rfind("read-only", 0) == 0) frac = static_cast<double>(k) / n;
     if (vs[vi].name.rfind("write-only", 0) == 0) frac = static_cast<double>(m) / n;
+    if (vs[vi].name.find("bytes:") == std::string::npos && frac != 1.0)
+      vs[vi].name += frac < 0.5 ? " (4/14)" : " (10/14)";
     const double gbs = bytes * frac / (med * 1e-3) / 1e9;
     std::printf("%-28s %10.1f %10.1f %10.1f %8.1f\n", vs[vi].name.c_str(), med * 1e3, mn * 1e3, gbs,
                 gbs / 80.0);
