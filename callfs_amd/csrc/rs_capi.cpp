@@ -164,7 +164,13 @@ struct HostBuf {
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
-    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return RS_E_NOMEM;
+    // Non-coherent: DMA into the default (coherent, fine-grained) pinned memory ran at
+    // 9 GB/s for 4 MiB D2H copies and 34-41 GB/s at 64 MiB, against 50 / 57 GB/s here
+    // (tools/host_ceilings.cpp). The host reads staging only after the
+    // slot's event has completed, so coherence during the copy is never needed.
+    static const unsigned flags =
+        std::getenv("CALLFS_RS_PINNED_COHERENT") ? hipHostMallocDefault : hipHostMallocNonCoherent;
+    if (hipHostMalloc(&p, n, flags) != hipSuccess) return RS_E_NOMEM;
     cap = n;
     return RS_OK;
   }
@@ -194,7 +200,16 @@ struct Slot {
   size_t off = 0, width = 0;  // and columns
 };
 
-constexpr int kSlots = 3;
+constexpr int kMaxSlots = 6;
+// Pipeline depth (slots per lane): CALLFS_RS_SLOTS overrides, 2..kMaxSlots.
+int pipeline_slots() {
+  static const int v = [] {
+    const char* e = std::getenv("CALLFS_RS_SLOTS");
+    const int x = e ? std::atoi(e) : 3;
+    return std::max(2, std::min(kMaxSlots, x));
+  }();
+  return v;
+}
 // Column chunk: about this many bytes over all n shards per pipeline step
 // (CALLFS_RS_CHUNK_BYTES overrides; DESIGN.md §6.3 has the sweep).
 size_t chunk_bytes() {
@@ -207,7 +222,7 @@ size_t chunk_bytes() {
 }
 
 struct Lane {
-  Slot slot[kSlots];
+  Slot slot[kMaxSlots];
 };
 
 struct Device {
@@ -465,6 +480,17 @@ int run_host1(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, In
                   [&](int, int i) { return out(i); });
 }
 
+// Runs [first, last] of consecutive values in an index list (sorted here).
+std::vector<std::pair<int, int>> index_runs(std::vector<int> v) {
+  std::sort(v.begin(), v.end());
+  std::vector<std::pair<int, int>> runs;
+  for (int x : v) {
+    if (!runs.empty() && runs.back().second + 1 == x) runs.back().second = x;
+    else runs.push_back({x, x});
+  }
+  return runs;
+}
+
 template <class InF, class OutF>
 int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const Tables>& tp,
                   size_t S, int batch, InF host_in, OutF host_out, int* stripe_status) {
@@ -497,10 +523,15 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   const size_t ncol = (S + cw - 1) / cw;
   const size_t nblk = (static_cast<size_t>(batch) + spc - 1) / spc;
   const size_t nchunks = ncol * nblk;
+  const int kSlots = pipeline_slots();
   const int nslots = static_cast<int>(std::min<size_t>(nchunks, kSlots));
   const MetaLayout ML = meta_layout(t, spc);
-  // small stripes move as one contiguous row range instead of one copy per shard
+  // Small stripes move as one contiguous row range (rows that are not inputs ride
+  // along). Larger chunks move one copy per run of consecutive shard indices: each copy
+  // on a stream costs ~9 us of gap, so one copy per shard was much slower than one per
+  // run.
   const bool coalesce = spitch <= (4u << 20);
+  const std::vector<std::pair<int, int>> in_runs = index_runs(ins), out_runs = index_runs(outs);
 
   for (int si = 0; si < nslots; ++si) {
     Slot& sl = L.slot[si];
@@ -567,10 +598,10 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
       HIPCHK(hipMemcpyAsync(d + cpitch * in_lo, h + cpitch * in_lo, bytes,
                             hipMemcpyHostToDevice, sl.stream));
     } else {
-      for (int b = 0; b < cnt; ++b)
-        for (int i : ins)
-          HIPCHK(hipMemcpyAsync(d + spitch * b + cpitch * i, h + spitch * b + cpitch * i, w,
-                                hipMemcpyHostToDevice, sl.stream));
+      for (const auto& r : in_runs)
+        HIPCHK(hipMemcpyAsync(d + cpitch * r.first, h + cpitch * r.first,
+                              cpitch * (r.second - r.first) + w, hipMemcpyHostToDevice,
+                              sl.stream));
     }
     if (verify) HIPCHK(hipMemsetAsync(dstatus, 0, sizeof(int) * cnt, sl.stream));
     HIPCHK(launch_groups(t, ML, cnt, meta, w, true, sl.stream, 1));
@@ -580,10 +611,10 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
         HIPCHK(hipMemcpyAsync(h + cpitch * out_lo, d + cpitch * out_lo, bytes,
                               hipMemcpyDeviceToHost, sl.stream));
       } else {
-        for (int b = 0; b < cnt; ++b)
-          for (int i : outs)
-            HIPCHK(hipMemcpyAsync(h + spitch * b + cpitch * i, d + spitch * b + cpitch * i, w,
-                                  hipMemcpyDeviceToHost, sl.stream));
+        for (const auto& r : out_runs)
+          HIPCHK(hipMemcpyAsync(h + cpitch * r.first, d + cpitch * r.first,
+                                cpitch * (r.second - r.first) + w, hipMemcpyDeviceToHost,
+                                sl.stream));
       }
     }
     if (verify)
