@@ -18,7 +18,8 @@
 //    no bank conflicts on random data, no per-lane table registers.
 //  * Input shards are consumed in pairs with the next pair's loads in flight, so
 //    register use does not grow with K (62 VGPRs at K=10, R=4: 8 waves/SIMD).
-//  * Ragged tails (S % 16) and unaligned shard pointers take the byte kernel.
+//  * Ragged tails (S % 16) take the byte kernel. Shard pointers need no alignment: 16-B
+//    global accesses at any byte address are legal on gfx950 (rs_kernels.hpp).
 #pragma once
 
 #include <algorithm>
@@ -456,7 +457,7 @@ void rs_apply_lds(ApplyArgs a) {
 // Dynamic LDS bytes of rs_apply_lds for K input shards and RT rows.
 inline size_t lds_bytes(int K, int RT) { return static_cast<size_t>(K) * 32 * (RT > 8 ? 16 : 8); }
 
-// One byte position per lane over [b0, S): ragged tails and unaligned pointers.
+// One byte position per lane over [b0, S): ragged tails (S % 16).
 template <int RT>
 __global__ __launch_bounds__(kBlock) void rs_apply_bytes(ApplyArgs a, uint64_t b0) {
   const uint64_t b = b0 + static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;

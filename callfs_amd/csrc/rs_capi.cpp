@@ -260,33 +260,24 @@ MetaLayout meta_layout(const Tables& t, int batch) {
 
 // Fill host staging for the meta buffer. shard_ptr(b, i) gives stripe b's shard i.
 template <class F>
-bool fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
+void fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
   std::memset(h + L.status_off, 0, sizeof(int) * static_cast<size_t>(batch));
   auto* in = reinterpret_cast<const uint8_t**>(h + L.in_off);
-  bool aligned = true;
-  auto note = [&](const void* p) { aligned &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   for (int b = 0; b < batch; ++b)
-    for (int i = 0; i < t.k; ++i) {
-      in[static_cast<size_t>(b) * t.k + i] = shard_ptr(b, t.valid[i]);
-      note(in[static_cast<size_t>(b) * t.k + i]);
-    }
+    for (int i = 0; i < t.k; ++i) in[static_cast<size_t>(b) * t.k + i] = shard_ptr(b, t.valid[i]);
   for (size_t gi = 0; gi < t.groups.size(); ++gi) {
     const Group& g = t.groups[gi];
     auto* out = reinterpret_cast<uint8_t**>(h + L.out_off[gi]);
     const size_t R = g.shard.size();
     for (int b = 0; b < batch; ++b)
-      for (size_t r = 0; r < R; ++r) {
-        out[b * R + r] = const_cast<uint8_t*>(shard_ptr(b, g.shard[r]));
-        note(out[b * R + r]);
-      }
+      for (size_t r = 0; r < R; ++r) out[b * R + r] = const_cast<uint8_t*>(shard_ptr(b, g.shard[r]));
     std::memcpy(h + L.tab_off[gi], g.tabs.data(), g.tabs.size() * sizeof(uint32_t));
     std::memcpy(h + L.ltab_off[gi], g.ltabs.data(), g.ltabs.size());
   }
-  return aligned;
 }
 
 hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_t* d, size_t S,
-                         bool aligned, hipStream_t s, int status_stride = 0) {
+                         hipStream_t s, int status_stride = 0) {
   for (size_t gi = 0; gi < t.groups.size(); ++gi) {
     const Group& g = t.groups[gi];
     ApplyArgs a{};
@@ -301,7 +292,7 @@ hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_
     a.K = t.k;
     a.R = static_cast<int>(g.shard.size());
     a.batch = batch;
-    hipError_t e = launch_apply(a, aligned, s);
+    hipError_t e = launch_apply(a, s);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -604,7 +595,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
                               sl.stream));
     }
     if (verify) HIPCHK(hipMemsetAsync(dstatus, 0, sizeof(int) * cnt, sl.stream));
-    HIPCHK(launch_groups(t, ML, cnt, meta, w, true, sl.stream, 1));
+    HIPCHK(launch_groups(t, ML, cnt, meta, w, sl.stream, 1));
     if (!outs.empty()) {
       if (coalesce) {
         const size_t bytes = spitch * (cnt - 1) + cpitch * (out_hi - out_lo) + w;
@@ -967,7 +958,6 @@ struct rs_plan {
   int device = 0;
   size_t S = 0;
   int batch = 0;
-  bool aligned = true;
   std::shared_ptr<const Tables> tables;
   MetaLayout layout;
   void* dmeta = nullptr;
@@ -1000,7 +990,7 @@ int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
   plan->layout = meta_layout(*t, batch);
   plan->bytes = algo_bytes(*t, S, batch);
   std::vector<uint8_t> h(plan->layout.total);
-  plan->aligned = fill_meta(*t, plan->layout, batch, h.data(), [&](int b, int i) {
+  fill_meta(*t, plan->layout, batch, h.data(), [&](int b, int i) {
     return static_cast<const uint8_t*>(shards[static_cast<size_t>(b) * n + i]);
   });
   HIPCHK(hipSetDevice(device));
@@ -1017,7 +1007,7 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
   if (!plan) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
   HIPCHK(launch_groups(*plan->tables, plan->layout, plan->batch,
-                       static_cast<uint8_t*>(plan->dmeta), plan->S, plan->aligned,
+                       static_cast<uint8_t*>(plan->dmeta), plan->S,
                        static_cast<hipStream_t>(stream), /*status_stride=*/1));
   return RS_OK;
 }

@@ -57,12 +57,12 @@ const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>
 
 }  // namespace
 
-hipError_t launch_apply(ApplyArgs a, bool aligned, hipStream_t stream) {
+hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
   uint64_t tail0 = 0;
-  if (aligned) {
+  if (!bytes_only) {
     a.nvec = a.S / 16;
     tail0 = a.nvec * 16;
     if (a.nvec) {

@@ -28,9 +28,12 @@ struct ApplyArgs {
   int batch;
 };
 
-// aligned: every in/out pointer is 16-byte aligned. Then [0, 16*floor(S/16)) runs on
-// the vector kernel and the ragged tail on the byte kernel; otherwise everything runs
-// on the byte kernel. Returns hipSuccess or the launch error.
-hipError_t launch_apply(ApplyArgs a, bool aligned, hipStream_t stream);
+// [0, 16*floor(S/16)) runs on a vector kernel and the ragged tail on the byte kernel,
+// whatever the pointers' alignment: gfx950 under ROCm (SH_MEM_CONFIG alignment mode
+// "unaligned") serves 16-byte global accesses at any byte address, and at odd shard
+// offsets (upstream Split layout of a contiguous object) that ran 4.7x the byte kernel
+// (DESIGN.md §5). bytes_only forces the byte kernel over all of [0, S) (kbench A/B).
+// Returns hipSuccess or the launch error.
+hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false);
 
 }  // namespace callfs

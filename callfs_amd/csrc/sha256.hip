@@ -6,8 +6,8 @@
 // wave, the rest of the wave idle, to spread few messages over more SIMDs). Rotates
 // lower to v_alignbit_b32, Ch/Maj/XOR3 to v_bitop3_b32, the sums to v_add3_u32. Each
 // lane issues the next block's four 16-B loads before the current block's 64 rounds.
-// Messages are read as dwordx4 when 16-B aligned, else byte by byte; padding and the
-// big-endian length follow FIPS 180-4 exactly (bit-exact with Go's crypto/sha256).
+// Messages are read as dwordx4 at any alignment; padding and the big-endian length
+// follow FIPS 180-4 exactly (bit-exact with Go's crypto/sha256).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -92,29 +92,19 @@ __global__ __launch_bounds__(64) void sha256_kernel(Sha256Args a) {
                     0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
   const uint64_t full = len / 64;
   uint32_t w[16];
-  if ((reinterpret_cast<uintptr_t>(msg) & 15u) == 0) {
-    uint4 q[4];
-    if (full) load_block16(msg, q);
-    for (uint64_t blk = 0; blk < full; ++blk) {
+  // 16-B loads at any byte address (legal on gfx950, rs_kernels.hpp): no byte path
+  uint4 q[4];
+  if (full) load_block16(msg, q);
+  for (uint64_t blk = 0; blk < full; ++blk) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        w[4 * i + 0] = be32(q[i].x);
-        w[4 * i + 1] = be32(q[i].y);
-        w[4 * i + 2] = be32(q[i].z);
-        w[4 * i + 3] = be32(q[i].w);
-      }
-      if (blk + 1 < full) load_block16(msg + 64 * (blk + 1), q);
-      compress(st, w);
+    for (int i = 0; i < 4; ++i) {
+      w[4 * i + 0] = be32(q[i].x);
+      w[4 * i + 1] = be32(q[i].y);
+      w[4 * i + 2] = be32(q[i].z);
+      w[4 * i + 3] = be32(q[i].w);
     }
-  } else {
-    for (uint64_t blk = 0; blk < full; ++blk) {
-      const uint8_t* p = msg + 64 * blk;
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        w[i] = (static_cast<uint32_t>(p[4 * i]) << 24) | (static_cast<uint32_t>(p[4 * i + 1]) << 16) |
-               (static_cast<uint32_t>(p[4 * i + 2]) << 8) | p[4 * i + 3];
-      compress(st, w);
-    }
+    if (blk + 1 < full) load_block16(msg + 64 * (blk + 1), q);
+    compress(st, w);
   }
   // tail: remaining bytes, 0x80, zeros, 64-bit big-endian bit length (1 or 2 blocks)
   const uint32_t rem = static_cast<uint32_t>(len - full * 64);

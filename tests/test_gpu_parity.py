@@ -301,21 +301,33 @@ def test_plan_decode_restores_and_verifies(native_lib, erase):
         assert dec.corrupt_stripes() == [3, 6]
 
 
-def test_plan_misaligned_pointers(native_lib):
-    """Shards aliasing one contiguous object (upstream Split layout) at odd S: byte
-    kernel path."""
+@pytest.mark.parametrize("k,m,S,off", [(10, 4, 100_003, 3), (3, 2, 349_526, 1),
+                                       (16, 4, 65_537, 15), (10, 9, 4_099, 7)])
+def test_plan_misaligned_pointers(native_lib, k, m, S, off):
+    """Shards aliasing one contiguous object (upstream Split layout) at odd S: every shard
+    starts at a different byte misalignment; the vector kernels (v_perm for k <= 3, LDS
+    otherwise, 16-row group for m = 9) read and write them with unaligned 16-B accesses,
+    the byte kernel takes the S % 16 tail. Encode, then a degraded decode, vs the oracle."""
     import torch
     from callfs_amd.device import Plan
-    k, m, S = 10, 4, 100_003
-    buf = torch.randint(0, 256, (k * S + m * S + 16,), dtype=torch.uint8, device="cuda:0")
-    base = buf.data_ptr() + 3
-    ptrs = [base + i * S for i in range(k + m)]
+    n = k + m
+    buf = torch.randint(0, 256, (n * S + 32,), dtype=torch.uint8, device="cuda:0")
+    base = buf.data_ptr() + off
+    ptrs = [base + i * S for i in range(n)]
     Plan(k, m, S, 1, ptrs).launch()
     torch.cuda.synchronize()
-    host = buf.cpu().numpy()[3:3 + (k + m) * S]
+    host = buf.cpu().numpy()[off:off + n * S].copy()
     want = cref.encode([host[i * S:(i + 1) * S] for i in range(k)], k, m)
     for j in range(m):
-        assert np.array_equal(host[(k + j) * S:(k + j + 1) * S], want[j])
+        assert np.array_equal(host[(k + j) * S:(k + j + 1) * S], want[j]), j
+    erase = [0, k - 1, k + m - 1][:m]
+    for i in erase:
+        buf[off + i * S:off + (i + 1) * S].zero_()
+    present = [i not in erase for i in range(n)]
+    dec = Plan(k, m, S, 1, ptrs, present=present)
+    dec.launch()
+    assert not dec.corrupt()
+    assert np.array_equal(buf.cpu().numpy()[off:off + n * S], host)
 
 
 def test_full_size_config_rs10_4_64mib_roundtrip(native_lib):

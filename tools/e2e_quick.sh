@@ -1,12 +1,10 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/e2e
-O=gpurun_out/e2e/coh.jsonl; rm -f $O
-for rep in 1 2; do for coh in 0 1; do
-  for cfg in "4096 1" "4096 8" "65536 1" "65536 8" "1048576 1" "1048576 8" "16777216 1" "67108864 1"; do
-    set -- $cfg
-    echo "{\"coherent\": $coh}" >> $O
-    if [ $coh = 1 ]; then export CALLFS_RS_PINNED_COHERENT=1; else unset CALLFS_RS_PINNED_COHERENT; fi
-    timeout -k 10 60 tools/e2e_native 16 4 $1 $2 0.7 0,5,16,19 >> $O || exit 1
-  done
-done; done
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ua
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+KB_BYTES=1 KB_KEEP="byte-kernel" timeout -k 10 120 tools/kbench 10 4 1048577 256 5 10 1 > gpurun_out/ua/rs10_4.log 2>&1 || exit $?
+KB_BYTES=1 KB_KEEP="byte-kernel" timeout -k 10 120 tools/kbench 10 4 6710887 64 5 10 1 > gpurun_out/ua/rs10_4_64m.log 2>&1 || exit $?
+KB_BYTES=1 KB_KEEP="byte-kernel" timeout -k 10 120 tools/kbench 3 2 349526 1024 5 10 1 > gpurun_out/ua/rs3_2.log 2>&1 || exit $?
+KB_BYTES=1 KB_KEEP="byte-kernel" timeout -k 10 120 tools/kbench 16 4 262145 256 5 10 1 > gpurun_out/ua/rs16_4.log 2>&1 || exit $?
+timeout -k 10 200 python3 tools/sha_bench.py > gpurun_out/ua/sha.json 2>&1 || exit $?
 echo ok

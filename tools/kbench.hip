@@ -212,8 +212,12 @@ int main(int argc, char** argv) {
   std::vector<Variant> vs;
   // what the library runs for this (K, R): rs_kernels.hip launch_apply's dispatch
   vs.push_back(Variant{"prod dispatch", [](const ApplyArgs& a, hipStream_t s) {
-                         CK(launch_apply(a, true, s));
+                         CK(launch_apply(a, s));
                        }});
+  if (std::getenv("KB_BYTES"))  // the byte kernel over the whole shard (unaligned-pointer dispatch)
+    vs.push_back(Variant{"byte-kernel dispatch", [](const ApplyArgs& a, hipStream_t s) {
+                           CK(launch_apply(a, s, /*bytes_only=*/true));
+                         }});
   switch (m) {  // v_perm kernel (runtime K) for this row count
     case 1: vs.push_back(make_variant<0, 1, Prod>("prod rtK nt")); break;
     case 2: vs.push_back(make_variant<0, 2, Prod>("prod rtK nt")); break;
