@@ -20,10 +20,14 @@ namespace callfs {
 // Threads: CALLFS_RS_COPY_THREADS, default min(8, hardware threads).
 class CopyPool {
  public:
+  // n bytes src -> dst; with dst2, the first n2 (<= n) of them also go to dst2 (a tee:
+  // the second copy reads the piece while it is still in cache).
   struct Seg {
     void* dst;
     const void* src;
     size_t n;
+    void* dst2 = nullptr;
+    size_t n2 = 0;
   };
 
   CopyPool() {
@@ -45,15 +49,18 @@ class CopyPool {
     size_t total = 0;
     for (const Seg& s : segs) total += s.n;
     if (workers_.empty() || total < kInline) {
-      for (const Seg& s : segs)
-        if (s.n) std::memcpy(s.dst, s.src, s.n);
+      for (const Seg& s : segs) copy(s);
       return;
     }
     Job job;
     for (const Seg& s : segs)
-      for (size_t o = 0; o < s.n; o += kPiece)
+      for (size_t o = 0; o < s.n; o += kPiece) {
+        const size_t len = std::min(kPiece, s.n - o);
+        const size_t len2 = s.dst2 && s.n2 > o ? std::min(len, s.n2 - o) : 0;
         job.pieces.push_back({static_cast<uint8_t*>(s.dst) + o,
-                              static_cast<const uint8_t*>(s.src) + o, std::min(kPiece, s.n - o)});
+                              static_cast<const uint8_t*>(s.src) + o, len,
+                              len2 ? static_cast<uint8_t*>(s.dst2) + o : nullptr, len2});
+      }
     {
       std::lock_guard<std::mutex> g(mu_);
       queue_.push_back(&job);
@@ -74,9 +81,13 @@ class CopyPool {
     int users = 0;  // workers inside work(); guarded by mu_
   };
 
+  static void copy(const Seg& s) {
+    if (s.n) std::memcpy(s.dst, s.src, s.n);
+    if (s.dst2 && s.n2) std::memcpy(s.dst2, s.src, std::min(s.n, s.n2));
+  }
+
   static void work(Job& j) {
-    for (size_t i; (i = j.next.fetch_add(1)) < j.pieces.size();)
-      std::memcpy(j.pieces[i].dst, j.pieces[i].src, j.pieces[i].n);
+    for (size_t i; (i = j.next.fetch_add(1)) < j.pieces.size();) copy(j.pieces[i]);
   }
 
   void unlink(Job* j) {

@@ -391,17 +391,40 @@ struct LaneGuard {
 // j-kSlots out. in(b, i)/out(b, i) give host buffers by stripe and shard index.
 // stripe_status (nullable, `batch` ints) receives 1 for stripes whose verify rows
 // mismatched. Returns RS_OK, RS_E_CORRUPT (some stripe mismatched) or an error.
+// Decode's join/trim target (codec.go:67-77): data shard i's column c belongs at
+// out[i*S + c] when that is below len (= min(originalSize, k*S)). The single-stripe
+// host path writes it while the columns pass through the copy pool (a tee on the
+// staging copies), instead of a separate k*S pass after the pipeline.
+struct Join {
+  uint8_t* out;
+  size_t len;
+  size_t S;  // full shard size (a column part's offset is added per part)
+  int k;
+  bool done = false;  // set when the pipeline wrote every join byte
+};
+
+// Tee target for shard i's columns [col, col+w) or {nullptr, 0}.
+std::pair<uint8_t*, size_t> join_span(const Join* j, int i, size_t col, size_t w) {
+  if (!j || i >= j->k) return {nullptr, 0};
+  const size_t pos = static_cast<size_t>(i) * j->S + col;
+  if (pos >= j->len) return {nullptr, 0};
+  return {j->out + pos, std::min(w, j->len - pos)};
+}
+
 template <class InF, class OutF>
 int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const Tables>& tp,
-                  size_t S, int batch, InF host_in, OutF host_out, int* stripe_status);
+                  size_t S, int batch, InF host_in, OutF host_out, int* stripe_status,
+                  const Join* join, size_t col0);
 
 template <class InF, class OutF>
 int run_on(rs_ctx* ctx, Device* dev, const std::shared_ptr<const Tables>& tp, size_t S,
-           int batch, InF host_in, OutF host_out, int* stripe_status) {
+           int batch, InF host_in, OutF host_out, int* stripe_status,
+           const Join* join = nullptr, size_t col0 = 0) {
   LaneGuard lg{ctx, dev, ctx->acquire(dev)};
   if (!lg.lane) return RS_E_HIP;
   const int rc =
-      run_host_impl(ctx, *lg.lane, dev->id, tp, S, batch, host_in, host_out, stripe_status);
+      run_host_impl(ctx, *lg.lane, dev->id, tp, S, batch, host_in, host_out, stripe_status,
+                    join, col0);
   if (rc != RS_OK && rc != RS_E_CORRUPT) {
     // never hand a lane with work in flight to the next caller
     for (Slot& sl : lg.lane->slot) {
@@ -432,14 +455,15 @@ int split_ways(const rs_ctx* ctx, size_t S, int n, int batch) {
 
 template <class InF, class OutF>
 int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, int batch,
-             InF host_in, OutF host_out, int* stripe_status = nullptr) {
+             InF host_in, OutF host_out, int* stripe_status = nullptr,
+             const Join* join = nullptr) {
   if (ctx->devs.empty()) return RS_E_HIP;
   const size_t nd = ctx->devs.size();
   const unsigned base = ctx->rr.fetch_add(1);
   const int ways = split_ways(ctx, S, tp->k + tp->m, batch);
   if (ways == 1)
     return run_on(ctx, ctx->devs[base % nd].get(), tp, S, batch, host_in, host_out,
-                  stripe_status);
+                  stripe_status, join, 0);
   // column parts [c[p], c[p+1]), 4 KiB aligned
   std::vector<size_t> c(ways + 1, 0);
   for (int p = 1; p < ways; ++p) c[p] = std::min(S, round_up(S / ways * p, 4096));
@@ -452,7 +476,7 @@ int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, int
       if (c[p + 1] <= c0) return;
       rc[p] = run_on(ctx, ctx->devs[(base + p) % nd].get(), tp, c[p + 1] - c0, 1,
                      [&](int b, int i) { return host_in(b, i) + c0; },
-                     [&](int b, int i) { return host_out(b, i) + c0; }, &flag[p]);
+                     [&](int b, int i) { return host_out(b, i) + c0; }, &flag[p], join, c0);
     });
   for (auto& t : th) t.join();
   int out = RS_OK;
@@ -466,9 +490,10 @@ int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, int
 
 // Single-stripe form used by the per-object entry points.
 template <class InF, class OutF>
-int run_host1(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, InF in, OutF out) {
+int run_host1(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, InF in, OutF out,
+              const Join* join = nullptr) {
   return run_host(ctx, tp, S, 1, [&](int, int i) { return in(i); },
-                  [&](int, int i) { return out(i); });
+                  [&](int, int i) { return out(i); }, nullptr, join);
 }
 
 // Runs [first, last] of consecutive values in an index list (sorted here).
@@ -484,7 +509,9 @@ std::vector<std::pair<int, int>> index_runs(std::vector<int> v) {
 
 template <class InF, class OutF>
 int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const Tables>& tp,
-                  size_t S, int batch, InF host_in, OutF host_out, int* stripe_status) {
+                  size_t S, int batch, InF host_in, OutF host_out, int* stripe_status,
+                  const Join* join, size_t col0) {
+  if (batch != 1) join = nullptr;  // only single-object decodes join
   const Tables& t = *tp;
   HIPCHK(hipSetDevice(device));
   const int n = t.k + t.m;
@@ -553,8 +580,11 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     segs.clear();
     auto* h = static_cast<uint8_t*>(sl.host.p);
     for (int b = 0; b < sl.count; ++b)
-      for (int i : outs)
-        segs.push_back({host_out(sl.b0 + b, i) + sl.off, h + spitch * b + cpitch * i, sl.width});
+      for (int i : outs) {
+        const auto tee = join_span(join, i, col0 + sl.off, sl.width);
+        segs.push_back({host_out(sl.b0 + b, i) + sl.off, h + spitch * b + cpitch * i, sl.width,
+                        tee.first, tee.second});
+      }
     ctx->pool.run(segs);
     if (verify) {
       const int* st = static_cast<const int*>(sl.hstat.p);
@@ -582,7 +612,11 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     dstatus = reinterpret_cast<int*>(meta + ML.status_off);
     segs.clear();
     for (int b = 0; b < cnt; ++b)
-      for (int i : ins) segs.push_back({h + spitch * b + cpitch * i, host_in(b0 + b, i) + off, w});
+      for (int i : ins) {
+        const auto tee = join_span(join, i, col0 + off, w);
+        segs.push_back({h + spitch * b + cpitch * i, host_in(b0 + b, i) + off, w, tee.first,
+                        tee.second});
+      }
     ctx->pool.run(segs);
     if (coalesce) {
       const size_t bytes = spitch * (cnt - 1) + cpitch * (in_hi - in_lo) + w;
@@ -646,7 +680,7 @@ int check_lens(int n, const size_t* lens, bool nilok, size_t* S, int* npresent) 
 
 // Shared by rs_reconstruct / rs_codec_decode. verify=true fuses upstream Verify.
 int reconstruct_host(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens,
-                     bool verify) {
+                     bool verify, Join* join = nullptr) {
   const int n = k + m;
   size_t S = 0;
   int np = 0;
@@ -661,9 +695,16 @@ int reconstruct_host(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* 
   auto t = ctx->cache.get(k, m, present, verify);
   if (!t) return RS_E_SINGULAR;
   if (t->groups.empty()) return RS_OK;
-  rc = run_host1(ctx, t, S, [&](int i) { return shards[i]; }, [&](int i) { return shards[i]; });
-  if (rc == RS_OK || rc == RS_E_CORRUPT)
+  if (join) {
+    join->S = S;
+    join->len = std::min(join->len, S * k);
+  }
+  rc = run_host1(ctx, t, S, [&](int i) { return shards[i]; }, [&](int i) { return shards[i]; },
+                 join);
+  if (rc == RS_OK || rc == RS_E_CORRUPT) {
     for (int i : t->missing) lens[i] = S;
+    if (join) join->done = true;
+  }
   return rc;
 }
 
@@ -829,11 +870,13 @@ int rs_codec_decode(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* l
   int rc = check_profile(k, m);
   if (rc) return rc;
   if (!ctx || !shards || !lens || original_size < 0 || (original_size && !out)) return RS_E_ARG;
-  rc = reconstruct_host(ctx, k, m, shards, lens, true);
+  Join join{out, static_cast<size_t>(original_size), 0, k};
+  rc = reconstruct_host(ctx, k, m, shards, lens, true, &join);
   if (rc) return rc;
   const size_t S = lens[0];
   if (static_cast<uint64_t>(S) * k < static_cast<uint64_t>(original_size))
     return RS_E_INSUFFICIENT;
+  if (join.done) return RS_OK;  // joined on the way through the pipeline
   size_t left = static_cast<size_t>(original_size);
   std::vector<CopyPool::Seg> segs;
   for (int i = 0; i < k && left; ++i) {

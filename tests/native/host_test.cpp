@@ -7,6 +7,7 @@
 //  4. CopyPool under concurrent callers
 #include <cstdio>
 #include <random>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -163,7 +164,7 @@ int main() {
     }
     CHECK(patterns == 1 + 9 + 36 + 84);
   }
-  // 4. copy pool: 6 concurrent callers, ragged segments
+  // 4. copy pool: 6 concurrent callers, ragged segments, tee prefixes
   {
     CopyPool pool;
     std::vector<std::thread> ts;
@@ -173,18 +174,26 @@ int main() {
         std::mt19937 rng(100 + t);
         for (int it = 0; it < 20; ++it) {
           const size_t nseg = 1 + rng() % 7;
-          std::vector<std::vector<uint8_t>> src(nseg), dst(nseg);
+          std::vector<std::vector<uint8_t>> src(nseg), dst(nseg), dst2(nseg);
+          std::vector<size_t> n2(nseg, 0);
           std::vector<CopyPool::Seg> segs;
           for (size_t s = 0; s < nseg; ++s) {
             const size_t len = rng() % (3u << 20);
             src[s].resize(len);
             for (size_t b = 0; b < len; b += 4093) src[s][b] = static_cast<uint8_t>(rng());
             dst[s].assign(len, 0xEE);
-            segs.push_back({dst[s].data(), src[s].data(), len});
+            // every other segment tees a prefix (decode's join) into a second buffer
+            if (s % 2 && len) n2[s] = 1 + rng() % len;
+            dst2[s].assign(n2[s] + 64, 0xDD);
+            segs.push_back({dst[s].data(), src[s].data(), len, n2[s] ? dst2[s].data() : nullptr,
+                            n2[s]});
           }
           pool.run(segs);
-          for (size_t s = 0; s < nseg; ++s)
+          for (size_t s = 0; s < nseg; ++s) {
             if (src[s] != dst[s]) bad++;
+            if (std::memcmp(dst2[s].data(), src[s].data(), n2[s]) != 0) bad++;
+            for (size_t b = n2[s]; b < dst2[s].size(); ++b) bad += dst2[s][b] != 0xDD;
+          }
         }
       });
     for (auto& th : ts) th.join();

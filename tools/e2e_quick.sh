@@ -1,10 +1,10 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ua
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/e2e
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
-KB_BYTES=1 KB_KEEP="byte-kernel" timeout -k 10 120 tools/kbench 10 4 1048577 256 5 10 1 > gpurun_out/ua/rs10_4.log 2>&1 || exit $?
-KB_BYTES=1 KB_KEEP="byte-kernel" timeout -k 10 120 tools/kbench 10 4 6710887 64 5 10 1 > gpurun_out/ua/rs10_4_64m.log 2>&1 || exit $?
-KB_BYTES=1 KB_KEEP="byte-kernel" timeout -k 10 120 tools/kbench 3 2 349526 1024 5 10 1 > gpurun_out/ua/rs3_2.log 2>&1 || exit $?
-KB_BYTES=1 KB_KEEP="byte-kernel" timeout -k 10 120 tools/kbench 16 4 262145 256 5 10 1 > gpurun_out/ua/rs16_4.log 2>&1 || exit $?
-timeout -k 10 200 python3 tools/sha_bench.py > gpurun_out/ua/sha.json 2>&1 || exit $?
+O=gpurun_out/e2e/join.jsonl; rm -f $O
+for L in 1048576 16777216 67108864; do timeout -k 10 60 tools/e2e_native 16 4 $L 1 1.0 0,5,16,19 >> $O || exit 1; done
+for L in 10485760 67108864 1073741824; do timeout -k 10 60 tools/e2e_native 10 4 $L 1 2.0 0,1,2,3 >> $O || exit 1; done
+timeout -k 10 60 tools/e2e_native 10 4 67108864 1 2.0 >> $O || exit 1
+timeout -k 10 60 tools/e2e_native 10 4 67108864 8 2.0 0,1,2,3 >> $O || exit 1
 echo ok
