@@ -816,23 +816,30 @@ int rs_codec_encode(rs_ctx* ctx, int k, int m, const uint8_t* data, size_t len,
   const size_t S = (len + k - 1) / k;
   const int n = k + m;
   if (out_cap < S * n) return RS_E_ARG;
-  if (shards_out != data) {
-    const bool overlap = shards_out < data + len && data < shards_out + S * n;
-    if (overlap) {
-      std::memmove(shards_out, data, len);
-    } else {
-      std::vector<CopyPool::Seg> segs{{shards_out, data, len}};
-      ctx->pool.run(segs);
-    }
-  }
-  std::memset(shards_out + len, 0, S * k - len);  // Split zero padding
-  *shard_size = S;
   uint8_t present[256];
   for (int i = 0; i < n; ++i) present[i] = i < k;
   auto t = ctx->cache.get(k, m, present, false);
   if (!t) return RS_E_SINGULAR;
-  return run_host1(ctx, t, S, [&](int i) { return shards_out + S * i; },
-                  [&](int i) { return shards_out + S * i; });
+  *shard_size = S;
+  const bool overlap = shards_out != data && shards_out < data + len && data < shards_out + S * n;
+  if (shards_out == data || overlap) {
+    if (overlap) std::memmove(shards_out, data, len);
+    std::memset(shards_out + len, 0, S * k - len);  // Split zero padding
+    return run_host1(ctx, t, S, [&](int i) { return shards_out + S * i; },
+                    [&](int i) { return shards_out + S * i; });
+  }
+  // Disjoint buffers: the partial last shard and its zero padding go to shards_out first;
+  // the full data shards are staged straight from `data`, and the staging copies tee
+  // them into shards_out (no separate object-sized copy).
+  const size_t full = len / S;
+  std::memcpy(shards_out + full * S, data + full * S, len - full * S);
+  std::memset(shards_out + len, 0, S * k - len);  // Split zero padding
+  Join tee{shards_out, full * S, S, k};
+  return run_host1(ctx, t, S,
+                   [&](int i) {
+                     return static_cast<size_t>(i) < full ? data + S * i : shards_out + S * i;
+                   },
+                   [&](int i) { return shards_out + S * i; }, &tee);
 }
 
 int rs_reconstruct(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens) {
