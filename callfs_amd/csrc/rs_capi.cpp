@@ -574,10 +574,12 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
 
   bool corrupt = false;
   std::vector<CopyPool::Seg> segs;
+  // Waits for the slot's chunk and appends its output copies to `segs` (run by the
+  // caller together with the next chunk's input copies: one pool job per step; the
+  // slot's input and output rows are disjoint).
   auto drain = [&](Slot& sl) -> int {
     if (!sl.pending) return RS_OK;
     HIPCHK(hipEventSynchronize(sl.done));
-    segs.clear();
     auto* h = static_cast<uint8_t*>(sl.host.p);
     for (int b = 0; b < sl.count; ++b)
       for (int i : outs) {
@@ -585,7 +587,6 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
         segs.push_back({host_out(sl.b0 + b, i) + sl.off, h + spitch * b + cpitch * i, sl.width,
                         tee.first, tee.second});
       }
-    ctx->pool.run(segs);
     if (verify) {
       const int* st = static_cast<const int*>(sl.hstat.p);
       for (int b = 0; b < sl.count; ++b)
@@ -601,6 +602,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   int* dstatus = nullptr;
   for (size_t j = 0; j < nchunks; ++j) {
     Slot& sl = L.slot[j % kSlots];
+    segs.clear();
     int rc = drain(sl);
     if (rc) return rc;
     const int b0 = static_cast<int>(j / ncol) * spc;
@@ -610,7 +612,6 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     auto* d = static_cast<uint8_t*>(sl.dev.p);
     auto* meta = static_cast<uint8_t*>(sl.meta.p);
     dstatus = reinterpret_cast<int*>(meta + ML.status_off);
-    segs.clear();
     for (int b = 0; b < cnt; ++b)
       for (int i : ins) {
         const auto tee = join_span(join, i, col0 + off, w);
@@ -653,8 +654,10 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     sl.width = w;
   }
   for (size_t j = nchunks > static_cast<size_t>(kSlots) ? nchunks - kSlots : 0; j < nchunks; ++j) {
+    segs.clear();
     int rc = drain(L.slot[j % kSlots]);
     if (rc) return rc;
+    ctx->pool.run(segs);
   }
   return corrupt ? RS_E_CORRUPT : RS_OK;
 }
