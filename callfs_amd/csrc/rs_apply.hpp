@@ -85,8 +85,10 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //   BS       threads per block; PD prefetch depth in input-shard pairs (1 or 2)
 //   ORD      tile order: 0 = a stripe's tiles consecutive, 1 = interleaved across all
 //            stripes, 2/3 = interleaved within groups of 8/32 stripes
+//   RING     LDS kernel input ring: 0 = three registers shifted each step (PD = 2);
+//            1 = PD+1 slots with the loop unrolled PD+1 times (static slot indices)
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
-          int PD_ = 1, int ORD_ = 0>
+          int PD_ = 1, int ORD_ = 0, int RING_ = 0>
 struct Policy {
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
@@ -96,6 +98,7 @@ struct Policy {
   static constexpr int BS = BS_;
   static constexpr int PD = PD_;
   static constexpr int ORD = ORD_;
+  static constexpr int RING = RING_;
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -426,14 +429,33 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[w][j] = lds_zero<RT>();
 
-    // ring of three shard vectors: shard i is consumed while i+1, i+2 load
-    uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = x0;
+    if constexpr (P::RING == 0) {
+      // ring of three shard vectors: shard i is consumed while i+1, i+2 load
+      uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = x0;
 #pragma unroll 1
-    for (int i = 0; i < K; ++i) {
-      if (i + 2 < K) x2 = ld(i + 2);
-      lds_mac<RT>(acc, x0, lds0 + static_cast<uint32_t>(i) * 32u * W);
-      x0 = x1;
-      x1 = x2;
+      for (int i = 0; i < K; ++i) {
+        if (i + 2 < K) x2 = ld(i + 2);
+        lds_mac<RT>(acc, x0, lds0 + static_cast<uint32_t>(i) * 32u * W);
+        x0 = x1;
+        x1 = x2;
+      }
+    } else {
+      // PD+1 slots, shard i in slot i % NR; shard i+PD loads into the slot shard i-1 left
+      constexpr int PD = P::PD, NR = P::PD + 1;
+      uint4 xr[NR];
+#pragma unroll
+      for (int s = 0; s < PD; ++s) xr[s] = s < K ? ld(s) : make_uint4(0, 0, 0, 0);
+#pragma unroll 1
+      for (int i0 = 0; i0 < K; i0 += NR) {
+#pragma unroll
+        for (int s = 0; s < NR; ++s) {
+          const int i = i0 + s;
+          if (i < K) {
+            if (i + PD < K) xr[(s + PD) % NR] = ld(i + PD);
+            lds_mac<RT>(acc, xr[s], lds0 + static_cast<uint32_t>(i) * 32u * W);
+          }
+        }
+      }
     }
 
     bool bad = false;

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <array>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 #include "rs_apply.hpp"
@@ -29,6 +30,14 @@ using ProdPolicy = dev::Policy<4, 1, true, true, false, 512, 2, 0>;
 // With k <= 3 the per-block table prologue does not pay (RS(3,2): 73.3 vs 77.5-79.9),
 // so those launches keep the v_perm kernel. One instance per R.
 using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
+// Row groups of 9..16 (16-byte table entries, 100-127 VGPRs, 4 waves/SIMD): fewer waves
+// hold fewer loads in flight, so they prefetch 4 input shards ahead through an unrolled
+// 5-slot ring. RS(10,12) 61.5 -> 68.0 %, RS(10,16) 63.2 -> 69.3 %, RS(20,16) 59.3 ->
+// 60.7 % of 8 TB/s (tools/kbench.hip, KB_RING). For R <= 8 the unrolled ring measured
+// 1-3 % slower than the shifted ring of three, so those keep LdsPolicy.
+using LdsWidePolicy = dev::Policy<2, 1, true, true, false, 512, 4, 0, 1>;
+template <int R>
+using LdsPolicyFor = typename std::conditional<(R > 8), LdsWidePolicy, LdsPolicy>::type;
 constexpr int kLdsMinRows = 5;
 constexpr int kLdsMinK = 4;
 constexpr int kPermMaxRows = 8;  // v_perm kernel instantiations (production: k <= 3, R <= 4)
@@ -43,7 +52,7 @@ constexpr auto vec_table(std::integer_sequence<int, Rs...>) {
 
 template <int... Rs>
 constexpr auto lds_table(std::integer_sequence<int, Rs...>) {
-  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsPolicy>...};
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsPolicyFor<Rs + 1>>...};
 }
 
 template <int... Rs>
@@ -77,6 +86,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
           });
         }
+        static_assert(LdsPolicy::BS == LdsWidePolicy::BS && LdsPolicy::U == LdsWidePolicy::U,
+                      "one grid shape for both LDS policies");
         const unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         hipLaunchKernelGGL(fn, dim3(gx), dim3(LdsPolicy::BS), lds, stream, a);
       } else {

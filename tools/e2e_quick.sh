@@ -1,10 +1,9 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/e2e
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ring2
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
-O=gpurun_out/e2e/onejob.jsonl; rm -f $O
-for L in 1048576 16777216 67108864; do timeout -k 10 60 tools/e2e_native 16 4 $L 1 1.0 0,5,16,19 >> $O || exit 1; done
-for L in 10485760 67108864 1073741824; do timeout -k 10 60 tools/e2e_native 10 4 $L 1 2.0 0,1,2,3 >> $O || exit 1; done
-CALLFS_E2E_ENCODER=1 timeout -k 10 60 tools/e2e_native 10 4 67108864 1 2.0 0,1,2,3 >> $O || exit 1
-timeout -k 10 60 tools/e2e_native 10 4 67108864 8 2.0 0,1,2,3 >> $O || exit 1
+export KB_KEEP="lds RT"
+for cfg in "10 9 1048576 128" "10 12 1048576 128" "10 16 1048576 128" "20 16 1048576 64" "32 16 1048576 64" "4 13 1048576 128" "10 4 1048576 256"; do
+  timeout -k 10 120 tools/kbench $cfg 5 10 > "gpurun_out/ring2/kb_${cfg// /_}.log" 2>&1 || exit $?
+done
 echo ok

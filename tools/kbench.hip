@@ -266,6 +266,23 @@ int main(int argc, char** argv) {
         launch_lds<1, L512w2>, launch_lds<2, L512w2>, launch_lds<3, L512w2>, launch_lds<4, L512w2>};
     vs.push_back(Variant{"lds prod-policy", [m](const ApplyArgs& a, hipStream_t s) { lds_r[m - 1](a, s); }});
   }
+  if (std::getenv("KB_RING")) {  // unrolled input ring of PD+1 slots (RING = 1)
+    using R2 = Policy<2, 1, true, true, false, 512, 2, 0, 1>;
+    using R3 = Policy<2, 1, true, true, false, 512, 3, 0, 1>;
+    using R4 = Policy<2, 1, true, true, false, 512, 4, 0, 1>;
+    using R6 = Policy<2, 1, true, true, false, 512, 6, 0, 1>;
+#define KB_RINGS(RT)                                                                                    \
+  vs.push_back(Variant{"lds ring pd2", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, R2>(a, s); }}); \
+  vs.push_back(Variant{"lds ring pd3", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, R3>(a, s); }}); \
+  vs.push_back(Variant{"lds ring pd4", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, R4>(a, s); }}); \
+  vs.push_back(Variant{"lds ring pd6", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, R6>(a, s); }});
+    switch (m) {
+      case 4: KB_RINGS(4) break;
+      case 8: KB_RINGS(8) break;
+      case 12: KB_RINGS(12) break;
+      case 16: KB_RINGS(16) break;
+    }
+  }
   if (rs10_4) vs.push_back(Variant{"read-only 10 streams (bytes: 10/14)", [](const ApplyArgs& a, hipStream_t s) {
                          const unsigned g = static_cast<unsigned>((a.nvec + 511) / 512 * a.batch);
                          hipLaunchKernelGGL((read_stream<10>), dim3(g), dim3(512), 0, s, a);
