@@ -117,7 +117,7 @@ def cpu_baseline(sb, k, m, erase, seconds, nstripes):
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "impl": f"oracle/rs_oracle.c orc_apply_simd ({cref.simd_kind()}, byte-range threads)",
+        "impl": f"oracle/rs_oracle.c orc_apply_simd ({cref.simd_kind()}, byte-range jobs on a persistent thread pool)",
         "sample": (f"{ns} stripes x RS({k},{m}) x {S} B shards, encode + decode(erase "
                    f"{sorted(erase)}: reconstruct + verify), {passes} passes in {el:.1f} s"),
         "parity_check": f"GPU parity == CPU port, bit-exact, on {ns} sampled stripes",

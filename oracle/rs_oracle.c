@@ -19,8 +19,9 @@
  *   orc_apply_simd    — the CPU baseline ("port"): the upstream SIMD strategy
  *                       (GFNI vgf2p8affineqb 8x8 bit-matrix per coefficient, or AVX2
  *                       split-nibble vpshufb tables, outputs held in registers while
- *                       inputs stream), split across threads by byte range like
- *                       upstream codeSomeShardsP.
+ *                       inputs stream), split by byte range like upstream
+ *                       codeSomeShardsP, the ranges run on a persistent thread pool
+ *                       (as goroutines reuse runtime threads).
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -188,10 +189,40 @@ int orc_verify(int k, int m, size_t S, const uint8_t* const* shards) {
 
 #define MAX_ROWS_SIMD 8
 
+/* Body with `rows` a compile-time constant at each call site below (always_inline), so
+ * the accumulators live in zmm registers like upstream's generated mulGFNI_{k}x{m}. */
+__attribute__((target("avx512f,avx512bw,gfni"), always_inline))
+static inline void apply_gfni_rows(const int rows, int k, const uint64_t* mats, size_t b0,
+                                   size_t b1, const uint8_t* const* in, uint8_t* const* out) {
+  size_t b = b0;
+  for (; b + 64 <= b1; b += 64) {
+    __m512i acc[MAX_ROWS_SIMD];
+    for (int r = 0; r < rows; r++) acc[r] = _mm512_setzero_si512();
+    for (int i = 0; i < k; i++) {
+      __m512i x = _mm512_loadu_si512((const void*)(in[i] + b));
+      for (int r = 0; r < rows; r++) {
+        __m512i A = _mm512_set1_epi64((long long)mats[(size_t)r * k + i]);
+        acc[r] = _mm512_xor_si512(acc[r], _mm512_gf2p8affine_epi64_epi8(x, A, 0));
+      }
+    }
+    for (int r = 0; r < rows; r++) _mm512_storeu_si512((void*)(out[r] + b), acc[r]);
+  }
+}
+
 __attribute__((target("avx512f,avx512bw,gfni")))
 static void apply_gfni_range(int rows, int k, const uint64_t* mats, size_t b0, size_t b1,
                              const uint8_t* const* in, uint8_t* const* out) {
   /* mats[r*k+i] = 8x8 GF(2) bit matrix multiplying by coef[r][i] in GF(2^8)/0x11D */
+  switch (rows) {
+    case 1: apply_gfni_rows(1, k, mats, b0, b1, in, out); return;
+    case 2: apply_gfni_rows(2, k, mats, b0, b1, in, out); return;
+    case 3: apply_gfni_rows(3, k, mats, b0, b1, in, out); return;
+    case 4: apply_gfni_rows(4, k, mats, b0, b1, in, out); return;
+    case 5: apply_gfni_rows(5, k, mats, b0, b1, in, out); return;
+    case 6: apply_gfni_rows(6, k, mats, b0, b1, in, out); return;
+    case 7: apply_gfni_rows(7, k, mats, b0, b1, in, out); return;
+    default: break;
+  }
   size_t b = b0;
   for (; b + 64 <= b1; b += 64) {
     __m512i acc[MAX_ROWS_SIMD];
@@ -280,7 +311,77 @@ static void run_range(const job_t* j) {
   }
 }
 
-static void* thread_main(void* p) { run_range((const job_t*)p); return NULL; }
+/* Persistent worker pool (the Go runtime reuses goroutine threads; spawning pthreads
+ * per call cost ~10-20 us each). Workers take job indices from an atomic counter; the
+ * caller takes jobs too and returns when every job is done. One call at a time. */
+#define POOL_MAX 256
+static struct {
+  pthread_mutex_t mu;
+  pthread_cond_t go, done;
+  int nworkers, gen, pending;
+  job_t* jobs;
+  int njobs;
+  int next;  /* guarded by mu */
+} g_pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER,
+            0, 0, 0, NULL, 0, 0};
+static pthread_mutex_t g_call = PTHREAD_MUTEX_INITIALIZER;
+
+static int pool_take(void) {
+  pthread_mutex_lock(&g_pool.mu);
+  int t = g_pool.next < g_pool.njobs ? g_pool.next++ : -1;
+  pthread_mutex_unlock(&g_pool.mu);
+  return t;
+}
+
+static void pool_finish(void) {
+  pthread_mutex_lock(&g_pool.mu);
+  if (--g_pool.pending == 0) pthread_cond_broadcast(&g_pool.done);
+  pthread_mutex_unlock(&g_pool.mu);
+}
+
+static void* pool_worker(void* arg) {
+  (void)arg;
+  int seen = 0;
+  for (;;) {
+    pthread_mutex_lock(&g_pool.mu);
+    while (g_pool.gen == seen) pthread_cond_wait(&g_pool.go, &g_pool.mu);
+    seen = g_pool.gen;
+    pthread_mutex_unlock(&g_pool.mu);
+    for (int t; (t = pool_take()) >= 0;) {
+      run_range(&g_pool.jobs[t]);
+      pool_finish();
+    }
+  }
+  return NULL;
+}
+
+static void pool_run(job_t* jobs, int njobs) {
+  pthread_mutex_lock(&g_call);
+  pthread_mutex_lock(&g_pool.mu);
+  while (g_pool.nworkers < njobs - 1 && g_pool.nworkers < POOL_MAX) {
+    pthread_t th;
+    if (pthread_create(&th, NULL, pool_worker, NULL) != 0) break;
+    pthread_detach(th);
+    g_pool.nworkers++;
+  }
+  g_pool.jobs = jobs;
+  g_pool.njobs = njobs;
+  g_pool.next = 0;
+  g_pool.pending = njobs;
+  g_pool.gen++;
+  pthread_cond_broadcast(&g_pool.go);
+  pthread_mutex_unlock(&g_pool.mu);
+  for (int t; (t = pool_take()) >= 0;) {
+    run_range(&jobs[t]);
+    pool_finish();
+  }
+  pthread_mutex_lock(&g_pool.mu);
+  while (g_pool.pending > 0) pthread_cond_wait(&g_pool.done, &g_pool.mu);
+  g_pool.jobs = NULL;
+  g_pool.njobs = 0;
+  pthread_mutex_unlock(&g_pool.mu);
+  pthread_mutex_unlock(&g_call);
+}
 
 /* CPU baseline entry point. Rows are processed MAX_ROWS_SIMD at a time. */
 void orc_apply_simd(int rows, int k, const uint8_t* coef, size_t S,
@@ -310,7 +411,6 @@ void orc_apply_simd(int rows, int k, const uint8_t* coef, size_t S,
     int njobs = (int)((S + per - 1) / per);
     if (njobs < 1) njobs = 1;
     job_t* jobs = (job_t*)calloc((size_t)njobs, sizeof(job_t));
-    pthread_t* th = (pthread_t*)calloc((size_t)njobs, sizeof(pthread_t));
     for (int t = 0; t < njobs; t++) {
       jobs[t].rows = rr; jobs[t].k = k; jobs[t].kind = kind;
       jobs[t].coef = cf; jobs[t].mats = mats; jobs[t].lo = lo; jobs[t].hi = hi;
@@ -318,9 +418,8 @@ void orc_apply_simd(int rows, int k, const uint8_t* coef, size_t S,
       jobs[t].b1 = (size_t)(t + 1) * per < S ? (size_t)(t + 1) * per : S;
       jobs[t].in = in; jobs[t].out = out + r0;
     }
-    for (int t = 1; t < njobs; t++) pthread_create(&th[t], NULL, thread_main, &jobs[t]);
-    run_range(&jobs[0]);
-    for (int t = 1; t < njobs; t++) pthread_join(th[t], NULL);
-    free(jobs); free(th); free(mats); free(lo); free(hi);
+    if (njobs == 1) run_range(&jobs[0]);
+    else pool_run(jobs, njobs);
+    free(jobs); free(mats); free(lo); free(hi);
   }
 }

@@ -1,7 +1,8 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/shift
-export KB_SHIFT=1 KB_KEEP="lds shift|lds prod-policy|lds bs512 (prod"
-for cfg in "10 4 1048576 256" "4 2 1048576 512" "10 8 1048576 256" "16 4 4194304 64"; do
-  timeout -k 10 120 tools/kbench $cfg 7 10 > "gpurun_out/shift/kb_${cfg// /_}.log" 2>&1 || exit $?
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/cpuab
+make -s -C oracle -B
+for rep in 1 2; do
+ORC_GFNI_GENERIC=1 timeout -k 10 200 python3 bench.py --steps 5 --warmup 2 --cpu-seconds 8 > gpurun_out/cpuab/generic_$rep.log 2>&1 || exit $?
+timeout -k 10 200 python3 bench.py --steps 5 --warmup 2 --cpu-seconds 8 > gpurun_out/cpuab/special_$rep.log 2>&1 || exit $?
 done
 echo ok
