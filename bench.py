@@ -58,6 +58,8 @@ def parse_args(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="CPU baseline time budget (0 disables)")
     p.add_argument("--cpu-stripes", type=int, default=16)
+    p.add_argument("--copy-ceiling", type=int, default=1,
+                   help="1: also time a device copy of the same bytes (roofline.copy_ceiling)")
     p.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
                    help="PMC-measured HBM bytes per launch (rocprofv3 --pmc), if present")
     return p.parse_args(argv)
@@ -122,6 +124,28 @@ def cpu_baseline(sb, k, m, erase, seconds, nstripes):
                    f"{sorted(erase)}: reconstruct + verify), {passes} passes in {el:.1f} s"),
         "parity_check": f"GPU parity == CPU port, bit-exact, on {ns} sampled stripes",
     }
+
+
+def copy_ceiling(total_bytes, dev, stream, reps=10):
+    """GB/s of a device copy moving the same bytes as one encode launch (half read, half
+    written), timed with HIP events on the launch stream; median of `reps`."""
+    n = total_bytes // 2
+    src = torch.empty(n, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    src.fill_(7)
+    with torch.cuda.stream(stream):
+        dst.copy_(src)
+        times = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            dst.copy_(src)
+            b.record(stream)
+            b.synchronize()
+            times.append(a.elapsed_time(b))
+    times.sort()
+    del src, dst
+    return 2 * n / (times[len(times) // 2] * 1e-3) / 1e9
 
 
 def load_traffic(path, cfg):
@@ -213,6 +237,7 @@ def main(argv=None):
     user_step = 2 * B * k * (S_obj if S_obj else S * world)
     value = args.steps * user_step / elapsed / 2**30
 
+    copy_gbs = copy_ceiling(enc.bytes, dev, stream) if args.copy_ceiling else None
     cfg = {"k": k, "m": m, "shard_bytes": S, "stripes": B}
     traffic, tsrc = load_traffic(args.traffic, cfg)
     achieved = enc.bytes / (enc_ms * 1e-3) / 1e9
@@ -252,6 +277,11 @@ def main(argv=None):
             "traffic": traffic,
             "traffic_source": tsrc,
             "algorithmic_bytes_per_launch": enc.bytes,
+            # also against a measured device copy of the same byte count
+            "copy_ceiling": (None if copy_gbs is None else
+                             {"kernel": "torch uint8 copy_ (read N + write N bytes)",
+                              "achieved": round(copy_gbs, 1),
+                              "frac": round(achieved / copy_gbs, 4)}),
         },
         "cpu_baseline": None,
     }
