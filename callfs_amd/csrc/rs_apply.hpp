@@ -84,7 +84,8 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //   PERSIST  grid-stride over tiles with a fixed grid instead of one tile per block
 //   BS       threads per block; PD prefetch depth in input-shard pairs (1 or 2)
 //   ORD      tile order: 0 = a stripe's tiles consecutive, 1 = interleaved across all
-//            stripes, 2/3 = interleaved within groups of 8/32 stripes
+//            stripes, 2/3/4/5 = interleaved within groups of 8/32/4/2 stripes (LDS
+//            kernel: 0 and 2..5)
 //   RING     LDS kernel input ring: 0 = three registers shifted each step (PD = 2);
 //            1 = PD+1 slots with the loop unrolled PD+1 times (static slot indices)
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
@@ -416,8 +417,21 @@ void rs_apply_lds(ApplyArgs a) {
   const uint32_t tps = static_cast<uint32_t>((a.nvec + BS - 1) / BS);
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
   for (uint32_t t = blockIdx.x; t < ntiles; t += ntiles) {
-    const uint32_t stripe = t / tps;
-    const uint64_t v0 = static_cast<uint64_t>(t - stripe * tps) * BS + threadIdx.x;
+    uint32_t stripe, tile;
+    if constexpr (P::ORD == 0) {
+      stripe = t / tps;
+      tile = t - stripe * tps;
+    } else {
+      // groups of G stripes whose tiles interleave (neighbouring blocks: same offset of
+      // different stripes)
+      constexpr uint32_t G = P::ORD == 2 ? 8 : (P::ORD == 3 ? 32 : (P::ORD == 4 ? 4 : 2));
+      const uint32_t per_group = G * tps;
+      const uint32_t g = t / per_group, r = t - g * per_group;
+      const uint32_t gsz = std::min<uint32_t>(G, static_cast<uint32_t>(a.batch) - g * G);
+      tile = r / gsz;
+      stripe = g * G + (r - tile * gsz);
+    }
+    const uint64_t v0 = static_cast<uint64_t>(tile) * BS + threadIdx.x;
     if (v0 >= a.nvec) continue;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;

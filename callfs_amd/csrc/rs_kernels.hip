@@ -38,6 +38,21 @@ using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
 using LdsWidePolicy = dev::Policy<2, 1, true, true, false, 512, 4, 0, 1>;
 template <int R>
 using LdsPolicyFor = typename std::conditional<(R > 8), LdsWidePolicy, LdsPolicy>::type;
+// Tile order across stripes for R <= 8 (Policy::ORD): neighbouring blocks on the same
+// column tile of 8 (G8) or 2 (G2) stripes instead of consecutive tiles of one stripe.
+// tools/kbench.hip KB_ORD, 9 rounds, % of 8 TB/s: S = 256 KiB (32 tiles per stripe)
+// RS(10,4) 70.8 -> 73.8 with G8; S = 4 MiB RS(16,4) 73.0 -> 74.6 and S = 6,710,887 (64 MiB
+// objects) RS(10,4) 73.0 -> 74.2 with G2; S = 1 MiB within +-0.6 of consecutive order; at
+// 16 MiB and 107 MB shards G2 / G8 lost up to 3.5, so those keep consecutive tiles.
+using LdsG8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 2>;
+using LdsG2Policy = dev::Policy<2, 1, true, true, false, 512, 2, 5>;
+enum class TileOrder { kConsecutive, kGroup8, kGroup2 };
+TileOrder lds_tile_order(uint64_t nvec) {
+  const uint64_t tps = (nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;
+  if (tps <= 64) return TileOrder::kGroup8;                  // S <= 512 KiB
+  if (tps >= 256 && tps <= 1024) return TileOrder::kGroup2;  // 2 MiB <= S <= 8 MiB
+  return TileOrder::kConsecutive;
+}
 constexpr int kLdsMinRows = 5;
 constexpr int kLdsMinK = 4;
 constexpr int kPermMaxRows = 8;  // v_perm kernel instantiations (production: k <= 3, R <= 4)
@@ -55,6 +70,11 @@ constexpr auto lds_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsPolicyFor<Rs + 1>>...};
 }
 
+template <class P, int... Rs>
+constexpr auto lds_order_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, P>...};
+}
+
 template <int... Rs>
 constexpr auto byte_table(std::integer_sequence<int, Rs...>) {
   return std::array<ByteFn, sizeof...(Rs)>{&dev::rs_apply_bytes<Rs + 1>...};
@@ -62,6 +82,8 @@ constexpr auto byte_table(std::integer_sequence<int, Rs...>) {
 
 const auto kVec = vec_table(std::make_integer_sequence<int, kPermMaxRows>{});
 const auto kLds = lds_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
+const auto kLdsG8 = lds_order_table<LdsG8Policy>(std::make_integer_sequence<int, 8>{});
+const auto kLdsG2 = lds_order_table<LdsG2Policy>(std::make_integer_sequence<int, 8>{});
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
 }  // namespace
@@ -79,6 +101,11 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         if (!a.ltabs) return hipErrorInvalidValue;
         const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
+        if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
+          const TileOrder o = lds_tile_order(a.nvec);
+          if (o == TileOrder::kGroup8) fn = kLdsG8[a.R - 1];
+          else if (o == TileOrder::kGroup2) fn = kLdsG2[a.R - 1];
+        }
         if (lds > (64u << 10)) {  // wide groups with many shards: opt in once per kernel
           static std::once_flag once[kMaxRowsPerLaunch];
           std::call_once(once[a.R - 1], [fn] {
@@ -86,8 +113,9 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
           });
         }
-        static_assert(LdsPolicy::BS == LdsWidePolicy::BS && LdsPolicy::U == LdsWidePolicy::U,
-                      "one grid shape for both LDS policies");
+        static_assert(LdsPolicy::BS == LdsWidePolicy::BS && LdsPolicy::U == LdsWidePolicy::U &&
+                          LdsG8Policy::BS == LdsPolicy::BS && LdsG2Policy::BS == LdsPolicy::BS,
+                      "one grid shape for every LDS policy");
         const unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         hipLaunchKernelGGL(fn, dim3(gx), dim3(LdsPolicy::BS), lds, stream, a);
       } else {

@@ -266,6 +266,16 @@ int main(int argc, char** argv) {
         launch_lds<1, L512w2>, launch_lds<2, L512w2>, launch_lds<3, L512w2>, launch_lds<4, L512w2>};
     vs.push_back(Variant{"lds prod-policy", [m](const ApplyArgs& a, hipStream_t s) { lds_r[m - 1](a, s); }});
   }
+  if (m == 4 && std::getenv("KB_ORD")) {  // LDS kernel tile orders across stripes
+    using O2 = Policy<2, 1, true, true, false, 512, 2, 2>;
+    using O3 = Policy<2, 1, true, true, false, 512, 2, 3>;
+    using O4 = Policy<2, 1, true, true, false, 512, 2, 4>;
+    using O5 = Policy<2, 1, true, true, false, 512, 2, 5>;
+    vs.push_back(Variant{"lds ord g8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O2>(a, s); }});
+    vs.push_back(Variant{"lds ord g32", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O3>(a, s); }});
+    vs.push_back(Variant{"lds ord g4", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O4>(a, s); }});
+    vs.push_back(Variant{"lds ord g2", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O5>(a, s); }});
+  }
   if (std::getenv("KB_RING")) {  // unrolled input ring of PD+1 slots (RING = 1)
     using R2 = Policy<2, 1, true, true, false, 512, 2, 0, 1>;
     using R3 = Policy<2, 1, true, true, false, 512, 3, 0, 1>;

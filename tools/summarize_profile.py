@@ -54,4 +54,7 @@ def main(src, dst, k=10, m=4, S=1 << 20, B=256, kernel="rs_apply_lds"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    # usage: summarize_profile.py <profile dir> <dst dir> [k m shard_bytes stripes]
+    a = sys.argv[1:]
+    extra = [int(x) for x in a[2:6]]
+    main(a[0], a[1], *extra)
