@@ -1,10 +1,6 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ord3
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -2 gpurun_out/pytest_gpu.log
-export KB_KEEP="lds prod-policy"
-for cfg in "10 4 262144 1024" "10 4 1048576 256" "16 4 4194304 64" "10 4 6710887 128" "10 4 16777216 32" "16 4 65536 4096"; do
-  timeout -k 10 120 tools/kbench $cfg 7 10 > "gpurun_out/ord3/kb_${cfg// /_}.log" 2>&1 || exit $?
-done
-timeout -k 10 300 python3 bench.py --cpu-seconds 0 > gpurun_out/ord3/bench.log 2>&1 || exit $?
+cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 python3 bench.py --shard-bytes 6710887 --stripes 256 --cpu-seconds 0 > gpurun_out/bench_cfg1.log 2>&1 || exit $?
+bash tools/profile.sh cfg1 --shard-bytes 6710887 --stripes 256 --copy-ceiling 0 || exit $?
+timeout -k 10 300 python3 tools/decode_sweep.py --shard-bytes 6710887 --stripes 128 --patterns "enc;;0,1,2,3;0,3,7,12;10,11,12,13" > gpurun_out/decode_cfg2.jsonl 2>&1 || exit $?
 echo ok
