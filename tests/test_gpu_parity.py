@@ -635,3 +635,62 @@ def test_plan_launches_replay_in_a_hip_graph(native_lib):
     g2.replay()
     torch.cuda.synchronize()
     assert dec.corrupt_stripes(s) == [2]
+
+
+# ---- randomized dispatch coverage ----------------------------------------------------
+
+def _random_cases(n=48, seed=0xD15):
+    """Seeded (k, m, S, batch, misalignment, erasures) draws spanning every dispatch path:
+    v_perm (k <= 3), LDS narrow (R <= 8) under each tile order (S <= 512 KiB: 8-stripe
+    interleave, 2..8 MiB: 2-stripe, else consecutive), LDS wide (R 9..16, 5-slot ring),
+    ragged tails and unaligned shard starts."""
+    rng = np.random.default_rng(seed)
+    sizes = [1, 15, 16, 17, 4095, 65_536 + 3, 262_144, 524_288 + 16, 1 << 20,
+             2 * (1 << 20) + 5, 4 << 20, 8 << 20, (8 << 20) + 4096]
+    cases = []
+    for c in range(n):
+        k = int(rng.choice([1, 2, 3, 4, 5, 10, 16, 20, 32]))
+        m = int(rng.choice([1, 2, 3, 4, 6, 8, 9, 12, 16]))
+        S = int(sizes[c % len(sizes)])
+        cap = (64 << 20) // (2 * (k + m))  # <= 64 MiB of shards per case, >= 2 stripes
+        if S > cap:
+            S = cap - c % 17
+        batch = max(2, min(4, (64 << 20) // (S * (k + m))))
+        off = int(rng.integers(0, 16)) if c % 3 == 0 else 0
+        ne = int(rng.integers(0, m + 1))
+        erase = sorted(rng.choice(k + m, size=ne, replace=False).tolist())
+        cases.append((k, m, S, batch, off, erase))
+    return cases
+
+
+@pytest.mark.parametrize("k,m,S,batch,off,erase", _random_cases())
+def test_random_plans_vs_oracle(native_lib, k, m, S, batch, off, erase):
+    """Device plans over a contiguous [stripe][shard] layout with pitch S + 16 (so a
+    nonzero `off` misaligns every shard differently): encode vs the C oracle on the first
+    and last stripe, then erase, decode, and require every stripe back bit-exactly with
+    no Verify flag."""
+    import torch
+    from callfs_amd.device import Plan
+    n = k + m
+    pitch = S + 16
+    buf = torch.randint(0, 256, (batch * n * pitch + 16,), dtype=torch.uint8, device="cuda:0")
+    base = buf.data_ptr() + off
+    ptrs = [base + (b * n + i) * pitch for b in range(batch) for i in range(n)]
+    enc = Plan(k, m, S, batch, ptrs)
+    enc.launch()
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()
+    view = lambda b, i: host[off + (b * n + i) * pitch: off + (b * n + i) * pitch + S]
+    for b in {0, batch - 1}:
+        want = cref.encode([view(b, i).copy() for i in range(k)], k, m, simd=True, nthreads=4)
+        for j in range(m):
+            assert np.array_equal(view(b, k + j), want[j]), (b, j)
+    ref = torch.from_numpy(host.copy()).to("cuda:0")
+    for b in range(batch):
+        for i in erase:
+            s0 = off + (b * n + i) * pitch
+            buf[s0:s0 + S].zero_()
+    dec = Plan(k, m, S, batch, ptrs, present=[i not in erase for i in range(n)])
+    dec.launch()
+    assert dec.corrupt_stripes() == []
+    assert torch.equal(buf, ref)
