@@ -63,6 +63,8 @@ SIGNATURES = {
     "rs_codec_encode": (_int, [_vp, _int, _int, _vp, _sz, _vp, _sz, ctypes.POINTER(_sz)]),
     "rs_codec_decode": (_int, [_vp, _int, _int, ctypes.POINTER(_vp), ctypes.POINTER(_sz), _vp,
                                _i64]),
+    "rs_host_alloc": (_int, [_vp, _sz, ctypes.POINTER(_vp)]),
+    "rs_host_free": (_int, [_vp, _vp]),
     "rs_encode": (_int, [_vp, _int, _int, _sz, ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
     "rs_reconstruct": (_int, [_vp, _int, _int, ctypes.POINTER(_vp), ctypes.POINTER(_sz)]),
     "rs_verify": (_int, [_vp, _int, _int, ctypes.POINTER(_vp), ctypes.POINTER(_sz),
@@ -128,6 +130,32 @@ class Context:
         if self.handle:
             lib.rs_shutdown(self.handle)
             self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PinnedBuffer:
+    """rs_host_alloc memory as a writable uint8 numpy array (`.array`). Host-memory calls
+    whose buffers all lie in such allocations DMA them directly (no staging copy)."""
+
+    def __init__(self, nbytes: int, context: "Context"):
+        import numpy as np
+        self.ctx = context
+        p = _vp()
+        check(lib.rs_host_alloc(context.handle, nbytes, ctypes.byref(p)), "rs_host_alloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.ptr))
+
+    def close(self) -> None:
+        if getattr(self, "ptr", None):
+            self.array = None
+            check(lib.rs_host_free(self.ctx.handle, ctypes.c_void_p(self.ptr)), "rs_host_free")
+            self.ptr = None
 
     def __del__(self):
         try:

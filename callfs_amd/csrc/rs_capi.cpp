@@ -307,13 +307,52 @@ uint64_t algo_bytes(const Tables& t, size_t S, int batch) {
 
 // ---- context ------------------------------------------------------------------------
 
+// Allocations made by rs_host_alloc: [base, base+size) ranges the host path may DMA
+// from / to directly.
+class PinnedRegistry {
+ public:
+  void add(void* p, size_t n) {
+    std::lock_guard<std::mutex> g(mu_);
+    ranges_[reinterpret_cast<uintptr_t>(p)] = n;
+  }
+  bool remove(void* p) {
+    std::lock_guard<std::mutex> g(mu_);
+    return ranges_.erase(reinterpret_cast<uintptr_t>(p)) == 1;
+  }
+  // true when [p, p+n) lies inside one registered allocation
+  bool contains(const void* p, size_t n) const {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = ranges_.upper_bound(a);
+    if (it == ranges_.begin()) return false;
+    --it;
+    return a >= it->first && a + n <= it->first + it->second;
+  }
+  bool empty() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return ranges_.empty();
+  }
+  std::vector<void*> all() const {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<void*> v;
+    for (const auto& r : ranges_) v.push_back(reinterpret_cast<void*>(r.first));
+    return v;
+  }
+
+ private:
+  mutable std::mutex mu_;
+  std::map<uintptr_t, size_t> ranges_;
+};
+
 struct rs_ctx {
   std::vector<std::unique_ptr<Device>> devs;
   std::atomic<unsigned> rr{0};
   TableCache cache;
   CopyPool pool;
+  PinnedRegistry pinned;
 
   ~rs_ctx() {
+    for (void* p : pinned.all()) (void)hipHostFree(p);  // buffers the caller did not free
     for (auto& d : devs) {
       (void)hipSetDevice(d->id);
       for (auto& l : d->lanes) {
@@ -551,6 +590,65 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   const bool coalesce = spitch <= (4u << 20);
   const std::vector<std::pair<int, int>> in_runs = index_runs(ins), out_runs = index_runs(outs);
 
+  // Zero-copy: when every caller buffer lies in rs_host_alloc memory (page-locked and
+  // mapped into the device's address space at the same address), the kernels read and
+  // write the caller's bytes over PCIe in one launch set over the whole call -- no
+  // staging copies, no chunk pipeline, nothing for the CPU but the join of present
+  // data shards. RS(10,4) 64 MiB: 43.7 GiB/s vs 36.7 for H2D + launch + D2H
+  // (tools/zerocopy_probe.py).
+  bool direct = !ctx->pinned.empty();
+  for (int b = 0; direct && b < batch; ++b) {
+    for (int i : ins) direct = direct && ctx->pinned.contains(host_in(b, i), S);
+    for (int i : outs) direct = direct && ctx->pinned.contains(host_out(b, i), S);
+  }
+  if (direct && join) direct = ctx->pinned.contains(join->out, join->len);
+  if (direct) {
+    Slot& sl = L.slot[0];
+    const MetaLayout DL = meta_layout(t, batch);
+    int rc;
+    if ((rc = sl.meta.ensure(DL.total)) || (rc = sl.hmeta.ensure(DL.total)) ||
+        (rc = sl.hstat.ensure(sizeof(int) * batch)))
+      return rc;
+    sl.meta_tables = nullptr;  // the staged path refills its tables next time
+    std::vector<char> is_out(n, 0);
+    for (int i : outs) is_out[i] = 1;
+    fill_meta(t, DL, batch, static_cast<uint8_t*>(sl.hmeta.p), [&](int b, int i) {
+      return is_out[i] ? static_cast<const uint8_t*>(host_out(b, i)) : host_in(b, i);
+    });
+    auto* meta = static_cast<uint8_t*>(sl.meta.p);
+    HIPCHK(hipMemcpyAsync(meta, sl.hmeta.p, DL.total, hipMemcpyHostToDevice, sl.stream));
+    HIPCHK(launch_groups(t, DL, batch, meta, S, sl.stream, 1));
+    if (verify)
+      HIPCHK(hipMemcpyAsync(sl.hstat.p, meta + DL.status_off, sizeof(int) * batch,
+                            hipMemcpyDeviceToHost, sl.stream));
+    HIPCHK(hipEventRecord(sl.done, sl.stream));
+    // decode's join: present data shards go to `out` while the kernels run,
+    // reconstructed ones once they have landed
+    auto join_segs = [&](bool present) {
+      std::vector<CopyPool::Seg> js_segs;
+      for (int i = 0; join && i < t.k; ++i) {
+        if (static_cast<bool>(is_out[i]) == present) continue;
+        const auto js = join_span(join, i, col0, S);
+        if (js.first)
+          js_segs.push_back({js.first, present ? host_in(0, i) : host_out(0, i), js.second});
+      }
+      ctx->pool.run(js_segs);
+    };
+    join_segs(true);
+    HIPCHK(hipEventSynchronize(sl.done));
+    join_segs(false);
+    bool corrupt = false;
+    if (verify) {
+      const int* st = static_cast<const int*>(sl.hstat.p);
+      for (int b = 0; b < batch; ++b)
+        if (st[b]) {
+          corrupt = true;
+          if (stripe_status) stripe_status[b] = 1;
+        }
+    }
+    return corrupt ? RS_E_CORRUPT : RS_OK;
+  }
+
   for (int si = 0; si < nslots; ++si) {
     Slot& sl = L.slot[si];
     int rc;
@@ -758,6 +856,25 @@ int rs_init(rs_ctx** out, unsigned device_mask) {
 void rs_shutdown(rs_ctx* ctx) { delete ctx; }
 
 int rs_device_count(const rs_ctx* ctx) { return ctx ? static_cast<int>(ctx->devs.size()) : 0; }
+
+int rs_host_alloc(rs_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !out || bytes == 0) return RS_E_ARG;
+  *out = nullptr;
+  void* p = nullptr;
+  // portable: every device of the context may use it. Coherent: the kernels read and
+  // write it in place (zero-copy), and the caller refills the same buffer between calls,
+  // so device caches must not keep its lines across launches.
+  if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess)
+    return RS_E_NOMEM;
+  ctx->pinned.add(p, bytes);
+  *out = p;
+  return RS_OK;
+}
+
+int rs_host_free(rs_ctx* ctx, void* p) {
+  if (!ctx || !p || !ctx->pinned.remove(p)) return RS_E_ARG;
+  return hipHostFree(p) == hipSuccess ? RS_OK : RS_E_HIP;
+}
 
 int rs_shard_size(int k, int m, int64_t len, int64_t* shard_size) {
   int rc = check_profile(k, m);

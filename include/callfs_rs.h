@@ -90,6 +90,20 @@ int rs_codec_encode(rs_ctx* ctx, int k, int m, const uint8_t* data, size_t len,
 int rs_codec_decode(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens,
                     uint8_t* out, int64_t original_size);
 
+/* ---- pinned host buffers: zero-copy staging -----------------------------------------
+ * rs_host_alloc returns `bytes` of page-locked host memory (page-aligned) that the
+ * host-memory entry points above and below DMA from and to directly. When every shard
+ * buffer of a call (and, for rs_codec_decode, `out`) lies inside such allocations, the
+ * call skips the library's CPU copy through its own pinned staging: H2D, kernels and
+ * D2H run on the caller's bytes, and the CPU only enqueues. A server reads request
+ * bodies and backend shards straight into these buffers. Calls with any
+ * other buffer use the copy-pool staging path as before. Free with rs_host_free
+ * (RS_E_ARG for a pointer rs_host_alloc did not return). No reference equivalent: Go's
+ * io.ReadAll allocations (post_file_enhanced.go:127, manager.go:473,530) are what it
+ * replaces on a ROCm build. */
+int rs_host_alloc(rs_ctx* ctx, size_t bytes, void** out);
+int rs_host_free(rs_ctx* ctx, void* p);
+
 /* ---- Encoder-level, host memory (reedsolomon.Encoder methods used by codec.go) -----
  * rs_encode:      enc.Encode(shards)      (codec.go:36)  data: k ptrs, parity: m ptrs, S bytes each
  * rs_reconstruct: enc.Reconstruct(shards) (codec.go:55)  same buffer/lens contract as rs_codec_decode

@@ -694,3 +694,108 @@ def test_random_plans_vs_oracle(native_lib, k, m, S, batch, off, erase):
     dec.launch()
     assert dec.corrupt_stripes() == []
     assert torch.equal(buf, ref)
+
+
+# ---- zero-copy staging: caller buffers in rs_host_alloc memory -----------------------
+
+def _pinned(n):
+    from callfs_amd import _native as N
+    return N.PinnedBuffer(n, N.default_context())
+
+
+@pytest.mark.parametrize("k,m,L", [(10, 4, (64 << 20) + 3), (16, 4, 5_000_000),
+                                   (3, 2, 1_048_576), (10, 9, 3_000_001)])
+def test_pinned_encode_and_decode_direct(native_lib, k, m, L):
+    """Object and shards in rs_host_alloc memory: rs_codec_encode, rs_encode and
+    rs_codec_decode (erasures + join into a pinned `out`) take the direct-DMA path; bytes
+    equal the oracle, and corruption is still reported."""
+    import ctypes
+    from callfs_amd import _native as N
+    ctx = N.default_context()
+    n = k + m
+    S = -(-L // k)
+    data = np.frombuffer(rnd(L, L), np.uint8)
+    src = _pinned(L)
+    src.array[:] = data
+    sh = _pinned(n * S)
+    ss = ctypes.c_size_t()
+    N.check(N.lib.rs_codec_encode(ctx.handle, k, m, src.ptr, L, sh.ptr, n * S, ctypes.byref(ss)))
+    assert ss.value == S
+    want = oracle_shards(data.tobytes(), k, m)
+    for i in range(n):
+        assert np.array_equal(sh.array[i * S:(i + 1) * S], want[i]), i
+    # rs_encode with data aliasing the pinned object (Split layout) and pinned parity
+    full = L // S
+    par = _pinned(m * S)
+    tail = _pinned(max(1, (k - full) * S))  # shards at and after the object's end
+    tail.array[:] = 0
+    tail.array[:L - full * S] = data[full * S:]
+    dptr = [src.ptr + i * S for i in range(full)] + [tail.ptr + i * S for i in range(k - full)]
+    N.check(N.lib.rs_encode(ctx.handle, k, m, S, (ctypes.c_void_p * k)(*dptr),
+                            (ctypes.c_void_p * m)(*[par.ptr + j * S for j in range(m)])))
+    for j in range(m):
+        assert np.array_equal(par.array[j * S:(j + 1) * S], want[k + j]), j
+    # decode: erase, reconstruct + verify + join into a pinned out
+    erase = [0, k - 1, n - 1][:m]
+    for i in erase:
+        sh.array[i * S:(i + 1) * S] = 0
+    lens = (ctypes.c_size_t * n)(*[0 if i in erase else S for i in range(n)])
+    ptrs = (ctypes.c_void_p * n)(*[sh.ptr + i * S for i in range(n)])
+    out = _pinned(L)
+    N.check(N.lib.rs_codec_decode(ctx.handle, k, m, ptrs, lens, out.ptr, L))
+    assert np.array_equal(out.array, data)
+    for i in erase:
+        assert np.array_equal(sh.array[i * S:(i + 1) * S], want[i]), i
+    # a flipped byte in a present parity beyond the first k is still caught
+    if m > 1:
+        sh.array[(n - 1) * S + 17] ^= 0x20
+        lens = (ctypes.c_size_t * n)(*[S] * n)
+        lens[1] = 0
+        assert N.lib.rs_codec_decode(ctx.handle, k, m, ptrs, lens, out.ptr, L) == N.RS_E_CORRUPT
+    for b in (src, sh, par, tail, out):
+        b.close()
+
+
+def test_pinned_buffers_reused_with_new_contents(native_lib):
+    """The server refills the same pinned buffers for every request: five encodes of
+    different data through the same buffers must each match the oracle (no stale lines
+    of an earlier call's bytes in device caches)."""
+    import ctypes
+    from callfs_amd import _native as N
+    ctx = N.default_context()
+    k, m, S = 10, 4, 1 << 20
+    src = _pinned(k * S)
+    par = _pinned(m * S)
+    dp = (ctypes.c_void_p * k)(*[src.ptr + i * S for i in range(k)])
+    pp = (ctypes.c_void_p * m)(*[par.ptr + j * S for j in range(m)])
+    for it in range(5):
+        src.array[:] = np.frombuffer(rnd(500 + it, k * S), np.uint8)
+        N.check(N.lib.rs_encode(ctx.handle, k, m, S, dp, pp))
+        want = cref.encode([src.array[i * S:(i + 1) * S] for i in range(k)], k, m, simd=True,
+                           nthreads=4)
+        for j in range(m):
+            assert np.array_equal(par.array[j * S:(j + 1) * S], want[j]), (it, j)
+    src.close()
+    par.close()
+
+
+def test_pinned_mixed_with_pageable_uses_staging(native_lib):
+    """One pageable output among pinned inputs: the call stays on the staging path and is
+    still bit-exact; freeing a pointer rs_host_alloc did not return is RS_E_ARG."""
+    import ctypes
+    from callfs_amd import _native as N
+    ctx = N.default_context()
+    k, m, S = 10, 4, 3 << 20
+    src = _pinned(k * S)
+    src.array[:] = np.frombuffer(rnd(9, k * S), np.uint8)
+    par = [bytearray(S) for _ in range(m)]
+    par_ptrs = [np.frombuffer(p, np.uint8).ctypes.data for p in par]
+    N.check(N.lib.rs_encode(ctx.handle, k, m, S,
+                            (ctypes.c_void_p * k)(*[src.ptr + i * S for i in range(k)]),
+                            (ctypes.c_void_p * m)(*par_ptrs)))
+    want = cref.encode([src.array[i * S:(i + 1) * S] for i in range(k)], k, m, simd=True,
+                       nthreads=4)
+    for j in range(m):
+        assert np.array_equal(np.frombuffer(par[j], np.uint8), want[j])
+    assert N.lib.rs_host_free(ctx.handle, ctypes.c_void_p(src.ptr + 1)) == N.RS_E_ARG
+    src.close()

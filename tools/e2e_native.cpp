@@ -9,17 +9,49 @@
 // parity only, as INTEGRATION.md's shim does) instead of rs_codec_encode.
 // CALLFS_E2E_BATCH=N: each call handles N objects through rs_encode_batch /
 // rs_reconstruct_batch (verify on) plus the per-object join copy.
+// CALLFS_E2E_PINNED=1: every buffer comes from rs_host_alloc (the server reading bodies
+// and shards into pinned memory), so calls take the zero-copy direct-DMA path.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <new>
 #include <random>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "callfs_rs.h"
+
+// Allocator for every buffer of the run: rs_host_alloc memory when CALLFS_E2E_PINNED is
+// set, plain heap otherwise.
+static rs_ctx* g_ctx = nullptr;
+static bool g_pinned = false;
+template <class T>
+struct MaybePinned {
+  using value_type = T;
+  MaybePinned() = default;
+  template <class U>
+  MaybePinned(const MaybePinned<U>&) {}
+  T* allocate(size_t n) {
+    if (!g_pinned) return static_cast<T*>(::operator new(n * sizeof(T)));
+    void* p = nullptr;
+    if (rs_host_alloc(g_ctx, std::max<size_t>(1, n * sizeof(T)), &p) != RS_OK) throw std::bad_alloc();
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t) {
+    if (!g_pinned) ::operator delete(p);
+    else rs_host_free(g_ctx, p);
+  }
+  template <class U>
+  bool operator==(const MaybePinned<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const MaybePinned<U>&) const { return false; }
+};
+using Bytes = std::vector<uint8_t, MaybePinned<uint8_t>>;
 
 int main(int argc, char** argv) {
   if (argc < 6) {
@@ -47,14 +79,17 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "rs_init failed\n");
     return 1;
   }
+  g_ctx = ctx;
+  g_pinned = std::getenv("CALLFS_E2E_PINNED") != nullptr;
   const size_t S = (L + k - 1) / k;
   struct Thr {
-    std::vector<uint8_t> src, enc, out;
-    std::vector<std::vector<uint8_t>> sh;
+    Bytes src, enc, out;
+    std::vector<Bytes> sh;
     long ops = 0;
     int err = 0;
   };
-  std::vector<Thr> th(T);
+  auto th_holder = std::make_unique<std::vector<Thr>>(T);
+  std::vector<Thr>& th = *th_holder;
   for (int t = 0; t < T; ++t) {
     std::mt19937_64 rng(1234 + t);
     th[t].src.resize(L);
@@ -63,7 +98,7 @@ int main(int argc, char** argv) {
     th[t].out.resize(L);
     size_t ss = 0;
     if (rs_codec_encode(ctx, k, m, th[t].src.data(), L, th[t].enc.data(), n * S, &ss) != RS_OK) return 1;
-    th[t].sh.assign(n, std::vector<uint8_t>(S));
+    th[t].sh.assign(n, Bytes(S));
     for (int i = 0; i < n; ++i) std::memcpy(th[t].sh[i].data(), th[t].enc.data() + S * i, S);
   }
   auto run = [&](bool encode) {
@@ -73,18 +108,18 @@ int main(int argc, char** argv) {
       th[t].ops = 0;
       ws.emplace_back([&, t] {
         Thr& me = th[t];
-        std::vector<uint8_t> enc2(n * S);
+        Bytes enc2(n * S);
         std::vector<uint8_t*> ptrs(n);
         std::vector<size_t> lens(n);
         // batch mode: every object shares the same input bytes, outputs are per object
         const int B = nb > 0 ? nb : 1;
-        std::vector<uint8_t> bout(nb > 0 ? static_cast<size_t>(B) * n * S : 0);
+        Bytes bout(nb > 0 ? static_cast<size_t>(B) * n * S : 0);
         std::vector<const uint8_t*> bdata(nb > 0 ? static_cast<size_t>(B) * k : 0);
         std::vector<uint8_t*> bpar(nb > 0 ? static_cast<size_t>(B) * m : 0);
         std::vector<uint8_t*> bsh(nb > 0 ? static_cast<size_t>(B) * n : 0);
         std::vector<size_t> bsz(B, S), blens(nb > 0 ? static_cast<size_t>(B) * n : 0);
         std::vector<int> bst(B);
-        std::vector<uint8_t> bjoin(nb > 0 ? L : 0);
+        Bytes bjoin(nb > 0 ? L : 0);
         while (!stop.load(std::memory_order_relaxed)) {
           int rc;
           if (nb > 0 && encode) {
@@ -165,7 +200,12 @@ int main(int argc, char** argv) {
   std::printf("{\"api\": \"%s\", \"k\": %d, \"m\": %d, \"object_bytes\": %zu, \"threads\": %d, "
               "\"batch\": %d, \"erase_count\": %zu, \"encode_gib_s\": %.3f, \"decode_gib_s\": %.3f, "
               "\"encode_calls\": %ld, \"decode_calls\": %ld, \"ok\": %s}\n",
-              nb > 0 ? "native-batch" : encoder_api ? "native-encoder" : "native", k, m, L, T, nb > 0 ? nb : 1, erase.size(), e.first, d.first, e.second, d.second, bad ? "false" : "true");
+              nb > 0 ? (g_pinned ? "native-batch-pinned" : "native-batch")
+                     : encoder_api ? (g_pinned ? "native-encoder-pinned" : "native-encoder")
+                                   : (g_pinned ? "native-pinned" : "native"),
+              k, m, L, T, nb > 0 ? nb : 1, erase.size(), e.first, d.first, e.second, d.second,
+              bad ? "false" : "true");
+  th_holder.reset();  // pinned buffers go back before the context
   rs_shutdown(ctx);
   return bad ? 1 : 0;
 }
