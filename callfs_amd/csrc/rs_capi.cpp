@@ -596,7 +596,12 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   // staging copies, no chunk pipeline, nothing for the CPU but the join of present
   // data shards. RS(10,4) 64 MiB: 43.7 GiB/s vs 36.7 for H2D + launch + D2H
   // (tools/zerocopy_probe.py).
-  bool direct = !ctx->pinned.empty();
+  static const unsigned long long zc_min = [] {
+    const char* e = std::getenv("CALLFS_RS_ZERO_COPY_MIN_BYTES");
+    return e ? std::strtoull(e, nullptr, 0) : (128ull << 10);  // crossover: 80-160 KiB
+  }();
+  bool direct = !ctx->pinned.empty() &&
+                static_cast<unsigned long long>(S) * n * batch >= zc_min;
   for (int b = 0; direct && b < batch; ++b) {
     for (int i : ins) direct = direct && ctx->pinned.contains(host_in(b, i), S);
     for (int i : outs) direct = direct && ctx->pinned.contains(host_out(b, i), S);
