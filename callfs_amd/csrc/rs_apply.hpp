@@ -84,8 +84,8 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //   PERSIST  grid-stride over tiles with a fixed grid instead of one tile per block
 //   BS       threads per block; PD prefetch depth in input-shard pairs (1 or 2)
 //   ORD      tile order: 0 = a stripe's tiles consecutive, 1 = interleaved across all
-//            stripes, 2/3/4/5 = interleaved within groups of 8/32/4/2 stripes (LDS
-//            kernel: 0 and 2..5)
+//            stripes, 2/3/4/5 = interleaved within groups of 8/32/4/2 stripes, 6/7/8/9 =
+//            interleaved across 8/32/16/64 column segments of one stripe (LDS kernel: 0, 2..9)
 //   RING     LDS kernel input ring: 0 = three registers shifted each step (PD = 2);
 //            1 = PD+1 slots with the loop unrolled PD+1 times (static slot indices)
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
@@ -421,6 +421,14 @@ void rs_apply_lds(ApplyArgs a) {
     if constexpr (P::ORD == 0) {
       stripe = t / tps;
       tile = t - stripe * tps;
+    } else if constexpr (P::ORD >= 6) {
+      // one stripe at a time, its columns cut into Q segments; neighbouring blocks take
+      // the same position of different segments (tiles past the last full round of Q
+      // keep their place, so the map stays a bijection)
+      constexpr uint32_t Q = P::ORD == 6 ? 8 : (P::ORD == 7 ? 32 : (P::ORD == 8 ? 16 : 64));
+      stripe = t / tps;
+      const uint32_t r = t - stripe * tps, seg = tps / Q;
+      tile = r < seg * Q ? (r % Q) * seg + r / Q : r;
     } else {
       // groups of G stripes whose tiles interleave (neighbouring blocks: same offset of
       // different stripes)

@@ -193,6 +193,7 @@ struct Slot {
   std::shared_ptr<const Tables> meta_tables;  // what `meta` currently holds
   size_t meta_pitch = 0;
   int meta_spc = 0;
+  int meta_tz = 0;  // shard_addr_tz of the pointers in `meta`
   void* meta_base = nullptr;
   HostBuf hstat;         // per-stripe verify flags of the chunk in flight
   bool pending = false;  // a chunk's outputs wait in `host`
@@ -259,8 +260,9 @@ MetaLayout meta_layout(const Tables& t, int batch) {
 }
 
 // Fill host staging for the meta buffer. shard_ptr(b, i) gives stripe b's shard i.
+// Returns shard_addr_tz over the shards stripe 0's launches touch (the tile-order key).
 template <class F>
-void fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
+int fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
   std::memset(h + L.status_off, 0, sizeof(int) * static_cast<size_t>(batch));
   auto* in = reinterpret_cast<const uint8_t**>(h + L.in_off);
   for (int b = 0; b < batch; ++b)
@@ -274,10 +276,15 @@ void fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F sh
     std::memcpy(h + L.tab_off[gi], g.tabs.data(), g.tabs.size() * sizeof(uint32_t));
     std::memcpy(h + L.ltab_off[gi], g.ltabs.data(), g.ltabs.size());
   }
+  std::vector<const void*> s0;
+  for (int i : t.valid) s0.push_back(shard_ptr(0, i));
+  for (const Group& g : t.groups)
+    for (int i : g.shard) s0.push_back(shard_ptr(0, i));
+  return shard_addr_tz(s0.data(), static_cast<int>(s0.size()));
 }
 
 hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_t* d, size_t S,
-                         hipStream_t s, int status_stride = 0) {
+                         hipStream_t s, int status_stride, int addr_tz) {
   for (size_t gi = 0; gi < t.groups.size(); ++gi) {
     const Group& g = t.groups[gi];
     ApplyArgs a{};
@@ -292,6 +299,7 @@ hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_
     a.K = t.k;
     a.R = static_cast<int>(g.shard.size());
     a.batch = batch;
+    a.addr_tz = addr_tz;
     hipError_t e = launch_apply(a, s);
     if (e != hipSuccess) return e;
   }
@@ -617,12 +625,12 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     sl.meta_tables = nullptr;  // the staged path refills its tables next time
     std::vector<char> is_out(n, 0);
     for (int i : outs) is_out[i] = 1;
-    fill_meta(t, DL, batch, static_cast<uint8_t*>(sl.hmeta.p), [&](int b, int i) {
+    const int tz = fill_meta(t, DL, batch, static_cast<uint8_t*>(sl.hmeta.p), [&](int b, int i) {
       return is_out[i] ? static_cast<const uint8_t*>(host_out(b, i)) : host_in(b, i);
     });
     auto* meta = static_cast<uint8_t*>(sl.meta.p);
     HIPCHK(hipMemcpyAsync(meta, sl.hmeta.p, DL.total, hipMemcpyHostToDevice, sl.stream));
-    HIPCHK(launch_groups(t, DL, batch, meta, S, sl.stream, 1));
+    HIPCHK(launch_groups(t, DL, batch, meta, S, sl.stream, 1, tz));
     if (verify)
       HIPCHK(hipMemcpyAsync(sl.hstat.p, meta + DL.status_off, sizeof(int) * batch,
                             hipMemcpyDeviceToHost, sl.stream));
@@ -664,8 +672,8 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     if (sl.meta_tables != tp || sl.meta_pitch != cpitch || sl.meta_spc != spc ||
         sl.meta_base != sl.dev.p) {
       auto* base = static_cast<uint8_t*>(sl.dev.p);
-      fill_meta(t, ML, spc, static_cast<uint8_t*>(sl.hmeta.p),
-                [&](int b, int i) { return base + spitch * b + cpitch * i; });
+      sl.meta_tz = fill_meta(t, ML, spc, static_cast<uint8_t*>(sl.hmeta.p),
+                             [&](int b, int i) { return base + spitch * b + cpitch * i; });
       HIPCHK(hipMemcpyAsync(sl.meta.p, sl.hmeta.p, ML.total, hipMemcpyHostToDevice, sl.stream));
       sl.meta_tables = tp;
       sl.meta_pitch = cpitch;
@@ -733,7 +741,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
                               sl.stream));
     }
     if (verify) HIPCHK(hipMemsetAsync(dstatus, 0, sizeof(int) * cnt, sl.stream));
-    HIPCHK(launch_groups(t, ML, cnt, meta, w, sl.stream, 1));
+    HIPCHK(launch_groups(t, ML, cnt, meta, w, sl.stream, 1, sl.meta_tz));
     if (!outs.empty()) {
       if (coalesce) {
         const size_t bytes = spitch * (cnt - 1) + cpitch * (out_hi - out_lo) + w;
@@ -1137,6 +1145,7 @@ struct rs_plan {
   MetaLayout layout;
   void* dmeta = nullptr;
   uint64_t bytes = 0;
+  int addr_tz = 0;
 };
 
 int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
@@ -1165,7 +1174,7 @@ int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
   plan->layout = meta_layout(*t, batch);
   plan->bytes = algo_bytes(*t, S, batch);
   std::vector<uint8_t> h(plan->layout.total);
-  fill_meta(*t, plan->layout, batch, h.data(), [&](int b, int i) {
+  plan->addr_tz = fill_meta(*t, plan->layout, batch, h.data(), [&](int b, int i) {
     return static_cast<const uint8_t*>(shards[static_cast<size_t>(b) * n + i]);
   });
   HIPCHK(hipSetDevice(device));
@@ -1183,7 +1192,7 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
   HIPCHK(hipSetDevice(plan->device));
   HIPCHK(launch_groups(*plan->tables, plan->layout, plan->batch,
                        static_cast<uint8_t*>(plan->dmeta), plan->S,
-                       static_cast<hipStream_t>(stream), /*status_stride=*/1));
+                       static_cast<hipStream_t>(stream), /*status_stride=*/1, plan->addr_tz));
   return RS_OK;
 }
 

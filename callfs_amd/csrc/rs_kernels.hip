@@ -38,19 +38,29 @@ using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
 using LdsWidePolicy = dev::Policy<2, 1, true, true, false, 512, 4, 0, 1>;
 template <int R>
 using LdsPolicyFor = typename std::conditional<(R > 8), LdsWidePolicy, LdsPolicy>::type;
-// Tile order across stripes for R <= 8 (Policy::ORD): neighbouring blocks on the same
-// column tile of 8 (G8) or 2 (G2) stripes instead of consecutive tiles of one stripe.
-// tools/kbench.hip KB_ORD, 9 rounds, % of 8 TB/s: S = 256 KiB (32 tiles per stripe)
-// RS(10,4) 70.8 -> 73.8 with G8; S = 4 MiB RS(16,4) 73.0 -> 74.6 and S = 6,710,887 (64 MiB
-// objects) RS(10,4) 73.0 -> 74.2 with G2; S = 1 MiB within +-0.6 of consecutive order; at
-// 16 MiB and 107 MB shards G2 / G8 lost up to 3.5, so those keep consecutive tiles.
+// Tile order for R <= 8 (Policy::ORD; tools/kbench.hip KB_ORD, tools/order_sweep.sh,
+// 9-15 rounds, % of 8 TB/s, DESIGN.md "Tile order"). Neighbouring blocks normally take
+// neighbouring column tiles of one stripe (consecutive). Up to 8 MiB shards it pays to
+// interleave the same column tile of G stripes instead: G8 for S <= 256 KiB (RS(10,4)
+// 256 KiB 70.8 -> 73.3), G2 from 256 KiB to 8 MiB (512 KiB 72.6 -> 77.6, RS(16,4) 1 MiB
+// 74.9 -> 78.8, RS(10,4) 1 MiB 78.8 -> 79.7, 64 MiB objects 73.0 -> 74.2-76.5). Above
+// 8 MiB, shards whose addresses differ by multiples of 8 MiB (addr_tz >= 23: power-of-two
+// pitches, 24/48 MiB) lose 5-13 points in consecutive order, which interleaving Q column
+// segments of the stripe recovers: Q16 for 16-32 MiB (RS(10,4) 16 MiB 67.6 -> 75.6,
+// RS(16,4) 16 MiB 64.4 -> 77.6, 32 MiB 74.0 -> 79.7), Q8 otherwise below 128 MiB (24 MiB
+// 70.9 -> 75.8, 48 MiB 68.9 -> 75.1, 64 MiB 69.3 -> 77.2). Pitches with few trailing
+// zeros (the 13-107 MB column slices of 1 GiB objects) and >= 128 MiB keep consecutive.
 using LdsG8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 2>;
 using LdsG2Policy = dev::Policy<2, 1, true, true, false, 512, 2, 5>;
-enum class TileOrder { kConsecutive, kGroup8, kGroup2 };
-TileOrder lds_tile_order(uint64_t nvec) {
+using LdsQ8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 6>;
+using LdsQ16Policy = dev::Policy<2, 1, true, true, false, 512, 2, 8>;
+enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16 };
+TileOrder lds_tile_order(uint64_t S, uint64_t nvec, int addr_tz) {
   const uint64_t tps = (nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;
-  if (tps <= 64) return TileOrder::kGroup8;                  // S <= 512 KiB
-  if (tps >= 256 && tps <= 1024) return TileOrder::kGroup2;  // 2 MiB <= S <= 8 MiB
+  if (tps <= 32) return TileOrder::kGroup8;    // S <= 256 KiB
+  if (tps <= 1024) return TileOrder::kGroup2;  // S <= 8 MiB
+  if (addr_tz >= 23 && S < (128ull << 20))
+    return addr_tz >= 24 && S <= (32ull << 20) ? TileOrder::kSeg16 : TileOrder::kSeg8;
   return TileOrder::kConsecutive;
 }
 constexpr int kLdsMinRows = 5;
@@ -84,6 +94,8 @@ const auto kVec = vec_table(std::make_integer_sequence<int, kPermMaxRows>{});
 const auto kLds = lds_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 const auto kLdsG8 = lds_order_table<LdsG8Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsG2 = lds_order_table<LdsG2Policy>(std::make_integer_sequence<int, 8>{});
+const auto kLdsQ8 = lds_order_table<LdsQ8Policy>(std::make_integer_sequence<int, 8>{});
+const auto kLdsQ16 = lds_order_table<LdsQ16Policy>(std::make_integer_sequence<int, 8>{});
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
 }  // namespace
@@ -102,9 +114,13 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
-          const TileOrder o = lds_tile_order(a.nvec);
-          if (o == TileOrder::kGroup8) fn = kLdsG8[a.R - 1];
-          else if (o == TileOrder::kGroup2) fn = kLdsG2[a.R - 1];
+          switch (lds_tile_order(a.S, a.nvec, a.addr_tz)) {
+            case TileOrder::kGroup8: fn = kLdsG8[a.R - 1]; break;
+            case TileOrder::kGroup2: fn = kLdsG2[a.R - 1]; break;
+            case TileOrder::kSeg8: fn = kLdsQ8[a.R - 1]; break;
+            case TileOrder::kSeg16: fn = kLdsQ16[a.R - 1]; break;
+            case TileOrder::kConsecutive: break;
+          }
         }
         if (lds > (64u << 10)) {  // wide groups with many shards: opt in once per kernel
           static std::once_flag once[kMaxRowsPerLaunch];
@@ -114,7 +130,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
           });
         }
         static_assert(LdsPolicy::BS == LdsWidePolicy::BS && LdsPolicy::U == LdsWidePolicy::U &&
-                          LdsG8Policy::BS == LdsPolicy::BS && LdsG2Policy::BS == LdsPolicy::BS,
+                          LdsG8Policy::BS == LdsPolicy::BS && LdsG2Policy::BS == LdsPolicy::BS &&
+                          LdsQ8Policy::BS == LdsPolicy::BS && LdsQ16Policy::BS == LdsPolicy::BS,
                       "one grid shape for every LDS policy");
         const unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         hipLaunchKernelGGL(fn, dim3(gx), dim3(LdsPolicy::BS), lds, stream, a);

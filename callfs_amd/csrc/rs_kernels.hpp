@@ -26,7 +26,20 @@ struct ApplyArgs {
   int K;
   int R;
   int batch;
+  // log2 of the largest power of two dividing every difference between the shard
+  // addresses of a stripe (shard_addr_tz); picks the LDS kernel's tile order. 0 = odd
+  // or unknown.
+  int addr_tz;
 };
+
+// addr_tz for a set of shard addresses: trailing zeros of the OR of their differences
+// from the first (63 for a single address).
+inline int shard_addr_tz(const void* const* p, int count) {
+  uint64_t d = 0;
+  for (int i = 1; i < count; ++i)
+    d |= reinterpret_cast<uintptr_t>(p[i]) ^ reinterpret_cast<uintptr_t>(p[0]);
+  return d ? __builtin_ctzll(d) : 63;
+}
 
 // [0, 16*floor(S/16)) runs on a vector kernel and the ragged tail on the byte kernel,
 // whatever the pointers' alignment: gfx950 under ROCm (SH_MEM_CONFIG alignment mode

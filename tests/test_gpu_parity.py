@@ -330,6 +330,44 @@ def test_plan_misaligned_pointers(native_lib, k, m, S, off):
     assert np.array_equal(buf.cpu().numpy()[off:off + n * S], host)
 
 
+@pytest.mark.parametrize("k,m,S,pitch,batch", [
+    (10, 4, (12 << 20) + 1000, 16 << 20, 2),  # addr_tz 24, S <= 32 MiB: 16 column segments
+    (6, 3, (20 << 20) + 77, 24 << 20, 1),     # addr_tz 23: 8 column segments
+    (10, 4, (40 << 20) + 5, 48 << 20, 1),     # addr_tz 24, S > 32 MiB: 8 segments
+    (10, 4, (9 << 20) + 3, (9 << 20) + 256, 2),  # few trailing zeros: consecutive tiles
+    (16, 4, 700_000, 1 << 20, 3),             # <= 8 MiB: 2-stripe interleave
+    (4, 4, 100_000, 1 << 17, 9),              # <= 256 KiB: 8-stripe interleave, ragged group
+])
+def test_plan_tile_orders_vs_oracle(native_lib, k, m, S, pitch, batch):
+    """Every LDS-kernel tile order of rs_kernels.hip lds_tile_order (keyed on the shard
+    size and the power-of-two factor of the shard address differences), with tiles per
+    stripe not a multiple of the segment count: encode and a degraded decode, bit-exact
+    against the oracle on the first and last stripe."""
+    import torch
+    from callfs_amd.device import Plan
+    n = k + m
+    buf = torch.empty(batch * n * pitch, dtype=torch.uint8, device="cuda:0")
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(S)
+    buf.random_(0, 256, generator=g)
+    ptrs = [buf.data_ptr() + (b * n + i) * pitch for b in range(batch) for i in range(n)]
+    Plan(k, m, S, batch, ptrs).launch()
+    torch.cuda.synchronize()
+    view = buf.view(batch, n, pitch)[:, :, :S]
+    want_all = view.cpu().numpy()
+    for b in {0, batch - 1}:
+        want = cref.encode([want_all[b, i] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(want_all[b, k + j], want[j]), (b, j)
+    erase = [0, k // 2, n - 1]
+    for i in erase:
+        view[:, i].fill_(0x5A)
+    dec = Plan(k, m, S, batch, ptrs, present=[i not in erase for i in range(n)])
+    dec.launch()
+    assert not dec.corrupt()
+    assert np.array_equal(view.cpu().numpy(), want_all)
+
+
 def test_full_size_config_rs10_4_64mib_roundtrip(native_lib):
     """configs[1]/[2] at full size: 256 objects of 64 MiB (S = 6,710,887; 22.4 GiB of
     shards in HBM). Encode the batch, erase 4 shards per pattern, decode, require every

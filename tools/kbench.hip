@@ -206,6 +206,11 @@ int main(int argc, char** argv) {
   a.K = k;
   a.R = m;
   a.batch = B;
+  {  // stripe 0's shard addresses, as rs_capi.cpp fill_meta computes it
+    std::vector<const void*> s0(in.begin(), in.begin() + k);
+    s0.insert(s0.end(), out.begin(), out.begin() + m);
+    a.addr_tz = shard_addr_tz(s0.data(), k + m);
+  }
 
   using namespace dev;
   using Prod = Policy<4, 1, true, true, false, 512, 2, 0>;  // = rs_kernels.hip ProdPolicy
@@ -275,6 +280,14 @@ int main(int argc, char** argv) {
     vs.push_back(Variant{"lds ord g32", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O3>(a, s); }});
     vs.push_back(Variant{"lds ord g4", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O4>(a, s); }});
     vs.push_back(Variant{"lds ord g2", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O5>(a, s); }});
+    using O6 = Policy<2, 1, true, true, false, 512, 2, 6>;
+    using O7 = Policy<2, 1, true, true, false, 512, 2, 7>;
+    vs.push_back(Variant{"lds ord q8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O6>(a, s); }});
+    vs.push_back(Variant{"lds ord q32", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O7>(a, s); }});
+    using O8 = Policy<2, 1, true, true, false, 512, 2, 8>;
+    using O9 = Policy<2, 1, true, true, false, 512, 2, 9>;
+    vs.push_back(Variant{"lds ord q16", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O8>(a, s); }});
+    vs.push_back(Variant{"lds ord q64", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O9>(a, s); }});
   }
   if (std::getenv("KB_RING")) {  // unrolled input ring of PD+1 slots (RING = 1)
     using R2 = Policy<2, 1, true, true, false, 512, 2, 0, 1>;
