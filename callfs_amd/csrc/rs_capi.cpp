@@ -398,8 +398,13 @@ struct rs_ctx {
         if (hipSetDevice(d->id) != hipSuccess) return nullptr;
         for (Slot& sl : l->slot)
           if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess ||
-              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
+              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+            for (Slot& s : l->slot) {  // a partly built lane is not kept: free what exists
+              if (s.done) (void)hipEventDestroy(s.done);
+              if (s.stream) (void)hipStreamDestroy(s.stream);
+            }
             return nullptr;
+          }
         d->lanes.push_back(std::move(l));
         return d->lanes.back().get();
       }

@@ -36,6 +36,12 @@ using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
 // 60.7 % of 8 TB/s (tools/kbench.hip, KB_RING). For R <= 8 the unrolled ring measured
 // 1-3 % slower than the shifted ring of three, so those keep LdsPolicy.
 using LdsWidePolicy = dev::Policy<2, 1, true, true, false, 512, 4, 0, 1>;
+// Wide groups hold 19-32 shard streams per stripe; from 2 MiB shards on, 8 interleaved
+// column segments beat consecutive tiles (tools/order_sweep.sh, KB_ORD, 9 rounds, % of
+// 8 TB/s: RS(10,12) 4 MiB 60.3 -> 66.9, RS(10,16) 16 MiB 58.0 -> 66.7; at 1 MiB all
+// orders are within 0.6 of each other, profiles/r01/tile_order/segments/ord_wide).
+using LdsWideQ8Policy = dev::Policy<2, 1, true, true, false, 512, 4, 6, 1>;
+constexpr uint64_t kWideSegMinTiles = 256;  // S >= 2 MiB
 template <int R>
 using LdsPolicyFor = typename std::conditional<(R > 8), LdsWidePolicy, LdsPolicy>::type;
 // Tile order for R <= 8 (Policy::ORD; tools/kbench.hip KB_ORD, tools/order_sweep.sh,
@@ -96,6 +102,11 @@ const auto kLdsG8 = lds_order_table<LdsG8Policy>(std::make_integer_sequence<int,
 const auto kLdsG2 = lds_order_table<LdsG2Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ8 = lds_order_table<LdsQ8Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ16 = lds_order_table<LdsQ16Policy>(std::make_integer_sequence<int, 8>{});
+template <class P, int... Rs>
+constexpr auto lds_wide_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 9, P>...};
+}
+const auto kLdsWideQ8 = lds_wide_table<LdsWideQ8Policy>(std::make_integer_sequence<int, 8>{});
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
 }  // namespace
@@ -121,17 +132,22 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
             case TileOrder::kSeg16: fn = kLdsQ16[a.R - 1]; break;
             case TileOrder::kConsecutive: break;
           }
+        } else if ((a.nvec + LdsWidePolicy::BS - 1) / LdsWidePolicy::BS >= kWideSegMinTiles) {
+          fn = kLdsWideQ8[a.R - 9];
         }
         if (lds > (64u << 10)) {  // wide groups with many shards: opt in once per kernel
+          // (only R > 8 gets here: both tile-order instances of that R opt in together)
           static std::once_flag once[kMaxRowsPerLaunch];
-          std::call_once(once[a.R - 1], [fn] {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
+          std::call_once(once[a.R - 1], [&a] {
+            for (VecFn f : {kLds[a.R - 1], kLdsWideQ8[a.R - 9]})
+              (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
           });
         }
         static_assert(LdsPolicy::BS == LdsWidePolicy::BS && LdsPolicy::U == LdsWidePolicy::U &&
                           LdsG8Policy::BS == LdsPolicy::BS && LdsG2Policy::BS == LdsPolicy::BS &&
-                          LdsQ8Policy::BS == LdsPolicy::BS && LdsQ16Policy::BS == LdsPolicy::BS,
+                          LdsQ8Policy::BS == LdsPolicy::BS && LdsQ16Policy::BS == LdsPolicy::BS &&
+                          LdsWideQ8Policy::BS == LdsPolicy::BS,
                       "one grid shape for every LDS policy");
         const unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         hipLaunchKernelGGL(fn, dim3(gx), dim3(LdsPolicy::BS), lds, stream, a);

@@ -337,6 +337,9 @@ def test_plan_misaligned_pointers(native_lib, k, m, S, off):
     (10, 4, (9 << 20) + 3, (9 << 20) + 256, 2),  # few trailing zeros: consecutive tiles
     (16, 4, 700_000, 1 << 20, 3),             # <= 8 MiB: 2-stripe interleave
     (4, 4, 100_000, 1 << 17, 9),              # <= 256 KiB: 8-stripe interleave, ragged group
+    (10, 12, (3 << 20) + 4112, 4 << 20, 2),   # 16-row group >= 2 MiB: 8 column segments
+    (10, 16, (1 << 20) + 48, 2 << 20, 1),     # 16-row group < 2 MiB: consecutive
+    (240, 16, (2 << 20) + 16, (2 << 20) + 256, 1),  # > 64 KiB of LDS tables, segments
 ])
 def test_plan_tile_orders_vs_oracle(native_lib, k, m, S, pitch, batch):
     """Every LDS-kernel tile order of rs_kernels.hip lds_tile_order (keyed on the shard

@@ -289,6 +289,23 @@ int main(int argc, char** argv) {
     vs.push_back(Variant{"lds ord q16", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O8>(a, s); }});
     vs.push_back(Variant{"lds ord q64", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O9>(a, s); }});
   }
+  if (std::getenv("KB_ORD") && m > 4) {  // tile orders for wider row groups (R 5..16)
+    using W0 = Policy<2, 1, true, true, false, 512, 4, 0, 1>;  // = rs_kernels.hip LdsWidePolicy
+    using W2 = Policy<2, 1, true, true, false, 512, 4, 5, 1>;
+    using W8 = Policy<2, 1, true, true, false, 512, 4, 2, 1>;
+    using WQ = Policy<2, 1, true, true, false, 512, 4, 6, 1>;
+    using N0 = Policy<2, 1, true, true, false, 512, 2, 0>;  // = LdsPolicy (R <= 8)
+#define KB_WORD(RT, P0)                                                                           \
+  vs.push_back(Variant{"lds ord consecutive", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, P0>(a, s); }}); \
+  vs.push_back(Variant{"lds ord wide g2", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, W2>(a, s); }}); \
+  vs.push_back(Variant{"lds ord wide g8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, W8>(a, s); }}); \
+  vs.push_back(Variant{"lds ord wide q8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, WQ>(a, s); }});
+    switch (m) {
+      case 8: KB_WORD(8, N0) break;
+      case 12: KB_WORD(12, W0) break;
+      case 16: KB_WORD(16, W0) break;
+    }
+  }
   if (std::getenv("KB_RING")) {  // unrolled input ring of PD+1 slots (RING = 1)
     using R2 = Policy<2, 1, true, true, false, 512, 2, 0, 1>;
     using R3 = Policy<2, 1, true, true, false, 512, 3, 0, 1>;
