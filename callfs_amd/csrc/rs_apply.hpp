@@ -405,46 +405,46 @@ void rs_apply_lds(ApplyArgs a) {
   // the launch passes R == RT; kept as a runtime stride so an RT instance can also
   // serve fewer rows (rows >= R are computed and dropped)
   const int R = a.R;
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + BS - 1) / BS);
+  const uint32_t t = blockIdx.x;  // one tile per block (vec_grid)
+  uint32_t stripe, tile;
+  if constexpr (P::ORD == 0) {
+    stripe = t / tps;
+    tile = t - stripe * tps;
+  } else if constexpr (P::ORD >= 6) {
+    // one stripe at a time, its columns cut into Q segments; neighbouring blocks take
+    // the same position of different segments (tiles past the last full round of Q
+    // keep their place, so the map stays a bijection)
+    constexpr uint32_t Q = P::ORD == 6 ? 8 : (P::ORD == 7 ? 32 : (P::ORD == 8 ? 16 : 64));
+    stripe = t / tps;
+    const uint32_t r = t - stripe * tps, seg = tps / Q;
+    tile = r < seg * Q ? (r % Q) * seg + r / Q : r;
+  } else {
+    // groups of G stripes whose tiles interleave (neighbouring blocks: same offset of
+    // different stripes)
+    constexpr uint32_t G = P::ORD == 2 ? 8 : (P::ORD == 3 ? 32 : (P::ORD == 4 ? 4 : 2));
+    const uint32_t per_group = G * tps;
+    const uint32_t g = t / per_group, r = t - g * per_group;
+    const uint32_t gsz = std::min<uint32_t>(G, static_cast<uint32_t>(a.batch) - g * G);
+    tile = r / gsz;
+    stripe = g * G + (r - tile * gsz);
+  }
+  const uint64_t v0 = static_cast<uint64_t>(tile) * BS + threadIdx.x;
+  const bool live = t < tps * static_cast<uint32_t>(a.batch) && v0 < a.nvec;
+  cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
+  cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
+  auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.ltabs);
     uint4* dst = reinterpret_cast<uint4*>(smem);
     for (int j = threadIdx.x; j < K * 2 * W; j += BS) dst[j] = src[j];
   }
   __syncthreads();
+  if (!live) return;
   // absolute LDS address of the tables (0 unless static LDS is ever added)
   const uint32_t lds0 = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)smem));
-  const uint32_t tps = static_cast<uint32_t>((a.nvec + BS - 1) / BS);
-  const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
-  for (uint32_t t = blockIdx.x; t < ntiles; t += ntiles) {
-    uint32_t stripe, tile;
-    if constexpr (P::ORD == 0) {
-      stripe = t / tps;
-      tile = t - stripe * tps;
-    } else if constexpr (P::ORD >= 6) {
-      // one stripe at a time, its columns cut into Q segments; neighbouring blocks take
-      // the same position of different segments (tiles past the last full round of Q
-      // keep their place, so the map stays a bijection)
-      constexpr uint32_t Q = P::ORD == 6 ? 8 : (P::ORD == 7 ? 32 : (P::ORD == 8 ? 16 : 64));
-      stripe = t / tps;
-      const uint32_t r = t - stripe * tps, seg = tps / Q;
-      tile = r < seg * Q ? (r % Q) * seg + r / Q : r;
-    } else {
-      // groups of G stripes whose tiles interleave (neighbouring blocks: same offset of
-      // different stripes)
-      constexpr uint32_t G = P::ORD == 2 ? 8 : (P::ORD == 3 ? 32 : (P::ORD == 4 ? 4 : 2));
-      const uint32_t per_group = G * tps;
-      const uint32_t g = t / per_group, r = t - g * per_group;
-      const uint32_t gsz = std::min<uint32_t>(G, static_cast<uint32_t>(a.batch) - g * G);
-      tile = r / gsz;
-      stripe = g * G + (r - tile * gsz);
-    }
-    const uint64_t v0 = static_cast<uint64_t>(tile) * BS + threadIdx.x;
-    if (v0 >= a.nvec) continue;
-    cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
-    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
-    auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
-
+  {
     AccT acc[4][4];
 #pragma unroll
     for (int w = 0; w < 4; ++w)
