@@ -50,7 +50,9 @@ def parse_args(argv=None):
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--m", type=int, default=4)
     p.add_argument("--shard-bytes", type=int, default=1 << 20)
-    p.add_argument("--stripes", type=int, default=256, help="stripes per GPU")
+    p.add_argument("--stripes", type=int, default=None,
+                   help="stripes per GPU (default 256; with --object-bytes: objects in total, "
+                        "default as many as keep ~16 GiB of shards resident on one GPU)")
     p.add_argument("--object-bytes", type=int, default=0,
                    help="configs[3] mode: objects of this size (e.g. 1073741824) split by byte "
                         "columns across the ranks (strong scaling); --stripes objects in total")
@@ -174,6 +176,10 @@ def main(argv=None):
     from callfs_amd.device import Plan, StripeBatch
 
     k, m, S, B = args.k, args.m, args.shard_bytes, args.stripes
+    if B is None:
+        B = 256
+        if args.object_bytes:  # configs[3]: 1 GiB objects -> 11 of them at N = 1
+            B = max(1, min(256, (16 << 30) // (-(-args.object_bytes // k) * (k + m))))
     scaling, S_obj = "weak", None
     if args.object_bytes:
         # configs[3]: each rank owns a 256-B-aligned byte-column slice of every object
