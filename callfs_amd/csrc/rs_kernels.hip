@@ -45,28 +45,38 @@ constexpr uint64_t kWideSegMinTiles = 256;  // S >= 2 MiB
 template <int R>
 using LdsPolicyFor = typename std::conditional<(R > 8), LdsWidePolicy, LdsPolicy>::type;
 // Tile order for R <= 8 (Policy::ORD; tools/kbench.hip KB_ORD, tools/order_sweep.sh,
-// 9-15 rounds, % of 8 TB/s, DESIGN.md "Tile order"). Neighbouring blocks normally take
-// neighbouring column tiles of one stripe (consecutive). Up to 8 MiB shards it pays to
-// interleave the same column tile of G stripes instead: G8 for S <= 256 KiB (RS(10,4)
-// 256 KiB 70.8 -> 73.3), G2 from 256 KiB to 8 MiB (512 KiB 72.6 -> 77.6, RS(16,4) 1 MiB
-// 74.9 -> 78.8, RS(10,4) 1 MiB 78.8 -> 79.7, 64 MiB objects 73.0 -> 74.2-76.5). Above
-// 8 MiB, shards whose addresses differ by multiples of 8 MiB (addr_tz >= 23: power-of-two
-// pitches, 24/48 MiB) lose 5-13 points in consecutive order, which interleaving Q column
-// segments of the stripe recovers: Q16 for 16-32 MiB (RS(10,4) 16 MiB 67.6 -> 75.6,
-// RS(16,4) 16 MiB 64.4 -> 77.6, 32 MiB 74.0 -> 79.7), Q8 otherwise below 128 MiB (24 MiB
-// 70.9 -> 75.8, 48 MiB 68.9 -> 75.1, 64 MiB 69.3 -> 77.2). Pitches with few trailing
-// zeros (the 13-107 MB column slices of 1 GiB objects) and >= 128 MiB keep consecutive.
+// 5-15 rounds, % of 8 TB/s, DESIGN.md "Tile order"). Neighbouring blocks normally take
+// neighbouring column tiles of one stripe (consecutive). For small shards it pays to
+// interleave the same column tile of G stripes instead: G8 up to 256 KiB (RS(10,4)
+// 256 KiB 70.8 -> 73.3-74.0, RS(16,4) 64 KiB 70.9 -> 73.5), G2 up to 1 MiB (512 KiB
+// 72.6 -> 77.6, RS(6,3) 1 MiB 73.7 -> 79.3, RS(10,4) 1 MiB 78.8 -> 79.7) and, for 14 or
+// more shard streams per stripe, up to 8 MiB (RS(16,4) 4 MiB 69.5 -> 75.2, 64 MiB
+// objects 74.6 -> 76.5); with fewer streams G2 loses 1-3.5 points at 4 MiB (RS(4,2)
+// 79.1 -> 75.6), so those keep consecutive tiles. Above 8 MiB, shards whose addresses
+// differ by multiples of 8 MiB (addr_tz >= 23: power-of-two pitches, 24/48 MiB) lose
+// 5-13 points in consecutive order once a stripe has 12 or more streams; interleaving
+// Q column segments of the stripe recovers it: Q16 for 16-32 MiB (RS(10,4) 16 MiB 67.6
+// -> 75.6, RS(16,4) 16 MiB 64.4 -> 77.6, RS(8,4) 32 MiB 71.5 -> 80.1), Q8 otherwise
+// below 128 MiB (24 MiB 70.9 -> 75.8, 48 MiB 68.9 -> 75.1, 64 MiB 69.3 -> 77.2). With
+// fewer streams Q16 hurts at 16 MiB (RS(4,2) 75.7 -> 67.9), so 6-11 streams keep
+// consecutive tiles up to 16 MiB and take Q8 above (RS(6,3) 32 MiB 75.1 -> 79.0).
+// Pitches with few trailing zeros (the 13-107 MB column slices of 1 GiB objects) and
+// >= 128 MiB keep consecutive tiles.
 using LdsG8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 2>;
 using LdsG2Policy = dev::Policy<2, 1, true, true, false, 512, 2, 5>;
 using LdsQ8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 6>;
 using LdsQ16Policy = dev::Policy<2, 1, true, true, false, 512, 2, 8>;
 enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16 };
-TileOrder lds_tile_order(uint64_t S, uint64_t nvec, int addr_tz) {
+TileOrder lds_tile_order(uint64_t S, uint64_t nvec, int addr_tz, int streams) {
   const uint64_t tps = (nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;
-  if (tps <= 32) return TileOrder::kGroup8;    // S <= 256 KiB
-  if (tps <= 1024) return TileOrder::kGroup2;  // S <= 8 MiB
-  if (addr_tz >= 23 && S < (128ull << 20))
-    return addr_tz >= 24 && S <= (32ull << 20) ? TileOrder::kSeg16 : TileOrder::kSeg8;
+  if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
+  if (tps <= 128 || (tps <= 1024 && streams >= 14)) return TileOrder::kGroup2;
+  if (tps <= 1024) return TileOrder::kConsecutive;  // S <= 8 MiB, few streams
+  if (addr_tz >= 23 && S < (128ull << 20)) {
+    if (streams >= 12)
+      return addr_tz >= 24 && S <= (32ull << 20) ? TileOrder::kSeg16 : TileOrder::kSeg8;
+    return S <= (16ull << 20) ? TileOrder::kConsecutive : TileOrder::kSeg8;
+  }
   return TileOrder::kConsecutive;
 }
 constexpr int kLdsMinRows = 5;
@@ -125,7 +135,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
-          switch (lds_tile_order(a.S, a.nvec, a.addr_tz)) {
+          switch (lds_tile_order(a.S, a.nvec, a.addr_tz, a.K + a.R)) {
             case TileOrder::kGroup8: fn = kLdsG8[a.R - 1]; break;
             case TileOrder::kGroup2: fn = kLdsG2[a.R - 1]; break;
             case TileOrder::kSeg8: fn = kLdsQ8[a.R - 1]; break;

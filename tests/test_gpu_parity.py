@@ -335,7 +335,8 @@ def test_plan_misaligned_pointers(native_lib, k, m, S, off):
     (6, 3, (20 << 20) + 77, 24 << 20, 1),     # addr_tz 23: 8 column segments
     (10, 4, (40 << 20) + 5, 48 << 20, 1),     # addr_tz 24, S > 32 MiB: 8 segments
     (10, 4, (9 << 20) + 3, (9 << 20) + 256, 2),  # few trailing zeros: consecutive tiles
-    (16, 4, 700_000, 1 << 20, 3),             # <= 8 MiB: 2-stripe interleave
+    (16, 4, 700_000, 1 << 20, 3),             # <= 1 MiB: 2-stripe interleave
+    (4, 2, (3 << 20) + 9, 4 << 20, 3),        # 1-8 MiB, 6 streams: consecutive
     (4, 4, 100_000, 1 << 17, 9),              # <= 256 KiB: 8-stripe interleave, ragged group
     (10, 12, (3 << 20) + 4112, 4 << 20, 2),   # 16-row group >= 2 MiB: 8 column segments
     (10, 16, (1 << 20) + 48, 2 << 20, 1),     # 16-row group < 2 MiB: consecutive
@@ -362,7 +363,7 @@ def test_plan_tile_orders_vs_oracle(native_lib, k, m, S, pitch, batch):
         want = cref.encode([want_all[b, i] for i in range(k)], k, m)
         for j in range(m):
             assert np.array_equal(want_all[b, k + j], want[j]), (b, j)
-    erase = [0, k // 2, n - 1]
+    erase = [0, k // 2, n - 1][:m]
     for i in erase:
         view[:, i].fill_(0x5A)
     dec = Plan(k, m, S, batch, ptrs, present=[i not in erase for i in range(n)])

@@ -271,37 +271,44 @@ int main(int argc, char** argv) {
         launch_lds<1, L512w2>, launch_lds<2, L512w2>, launch_lds<3, L512w2>, launch_lds<4, L512w2>};
     vs.push_back(Variant{"lds prod-policy", [m](const ApplyArgs& a, hipStream_t s) { lds_r[m - 1](a, s); }});
   }
-  if (m == 4 && std::getenv("KB_ORD")) {  // LDS kernel tile orders across stripes
+  if ((m == 2 || m == 3 || m == 4 || m == 8) && std::getenv("KB_ORD")) {  // LDS kernel tile orders
+    using O0 = Policy<2, 1, true, true, false, 512, 2, 0>;
     using O2 = Policy<2, 1, true, true, false, 512, 2, 2>;
     using O3 = Policy<2, 1, true, true, false, 512, 2, 3>;
     using O4 = Policy<2, 1, true, true, false, 512, 2, 4>;
     using O5 = Policy<2, 1, true, true, false, 512, 2, 5>;
-    vs.push_back(Variant{"lds ord g8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O2>(a, s); }});
-    vs.push_back(Variant{"lds ord g32", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O3>(a, s); }});
-    vs.push_back(Variant{"lds ord g4", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O4>(a, s); }});
-    vs.push_back(Variant{"lds ord g2", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O5>(a, s); }});
     using O6 = Policy<2, 1, true, true, false, 512, 2, 6>;
     using O7 = Policy<2, 1, true, true, false, 512, 2, 7>;
-    vs.push_back(Variant{"lds ord q8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O6>(a, s); }});
-    vs.push_back(Variant{"lds ord q32", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O7>(a, s); }});
     using O8 = Policy<2, 1, true, true, false, 512, 2, 8>;
     using O9 = Policy<2, 1, true, true, false, 512, 2, 9>;
-    vs.push_back(Variant{"lds ord q16", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O8>(a, s); }});
-    vs.push_back(Variant{"lds ord q64", [](const ApplyArgs& a, hipStream_t s) { launch_lds<4, O9>(a, s); }});
+#define KB_ORDS(RT)                                                                                  \
+  vs.push_back(Variant{"lds ord consec", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, O0>(a, s); }}); \
+  vs.push_back(Variant{"lds ord g8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, O2>(a, s); }}); \
+  vs.push_back(Variant{"lds ord g32", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, O3>(a, s); }}); \
+  vs.push_back(Variant{"lds ord g4", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, O4>(a, s); }}); \
+  vs.push_back(Variant{"lds ord g2", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, O5>(a, s); }}); \
+  vs.push_back(Variant{"lds ord q8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, O6>(a, s); }}); \
+  vs.push_back(Variant{"lds ord q32", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, O7>(a, s); }}); \
+  vs.push_back(Variant{"lds ord q16", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, O8>(a, s); }}); \
+  vs.push_back(Variant{"lds ord q64", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, O9>(a, s); }});
+    switch (m) {
+      case 2: KB_ORDS(2) break;
+      case 3: KB_ORDS(3) break;
+      case 4: KB_ORDS(4) break;
+      case 8: KB_ORDS(8) break;
+    }
   }
-  if (std::getenv("KB_ORD") && m > 4) {  // tile orders for wider row groups (R 5..16)
+  if (std::getenv("KB_ORD") && m > 8) {  // tile orders for wider row groups (R 9..16)
     using W0 = Policy<2, 1, true, true, false, 512, 4, 0, 1>;  // = rs_kernels.hip LdsWidePolicy
     using W2 = Policy<2, 1, true, true, false, 512, 4, 5, 1>;
     using W8 = Policy<2, 1, true, true, false, 512, 4, 2, 1>;
     using WQ = Policy<2, 1, true, true, false, 512, 4, 6, 1>;
-    using N0 = Policy<2, 1, true, true, false, 512, 2, 0>;  // = LdsPolicy (R <= 8)
 #define KB_WORD(RT, P0)                                                                           \
   vs.push_back(Variant{"lds ord consecutive", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, P0>(a, s); }}); \
   vs.push_back(Variant{"lds ord wide g2", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, W2>(a, s); }}); \
   vs.push_back(Variant{"lds ord wide g8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, W8>(a, s); }}); \
   vs.push_back(Variant{"lds ord wide q8", [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, WQ>(a, s); }});
     switch (m) {
-      case 8: KB_WORD(8, N0) break;
       case 12: KB_WORD(12, W0) break;
       case 16: KB_WORD(16, W0) break;
     }
