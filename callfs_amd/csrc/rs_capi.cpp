@@ -181,6 +181,13 @@ struct HostBuf {
   }
 };
 
+// Layout facts the kernel dispatch keys its tile order on (ApplyArgs addr_tz,
+// stripe_stride).
+struct LayoutHint {
+  int addr_tz = 0;
+  uint64_t stripe_stride = 0;
+};
+
 // One pipeline stage of the host-memory path: a stream, a pinned chunk buffer and its
 // device mirror ([n][cpitch]), and the pointer/coefficient tables for launches on it.
 struct Slot {
@@ -193,7 +200,7 @@ struct Slot {
   std::shared_ptr<const Tables> meta_tables;  // what `meta` currently holds
   size_t meta_pitch = 0;
   int meta_spc = 0;
-  int meta_tz = 0;  // shard_addr_tz of the pointers in `meta`
+  LayoutHint meta_hint;  // of the pointers in `meta`
   void* meta_base = nullptr;
   HostBuf hstat;         // per-stripe verify flags of the chunk in flight
   bool pending = false;  // a chunk's outputs wait in `host`
@@ -260,9 +267,10 @@ MetaLayout meta_layout(const Tables& t, int batch) {
 }
 
 // Fill host staging for the meta buffer. shard_ptr(b, i) gives stripe b's shard i.
-// Returns shard_addr_tz over the shards stripe 0's launches touch (the tile-order key).
+// Returns the layout hint: shard_addr_tz over the shards stripe 0's launches touch, and
+// the stripe stride when every stripe sits at the same distance from the previous one.
 template <class F>
-int fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
+LayoutHint fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
   std::memset(h + L.status_off, 0, sizeof(int) * static_cast<size_t>(batch));
   auto* in = reinterpret_cast<const uint8_t**>(h + L.in_off);
   for (int b = 0; b < batch; ++b)
@@ -280,11 +288,21 @@ int fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F sha
   for (int i : t.valid) s0.push_back(shard_ptr(0, i));
   for (const Group& g : t.groups)
     for (int i : g.shard) s0.push_back(shard_ptr(0, i));
-  return shard_addr_tz(s0.data(), static_cast<int>(s0.size()));
+  LayoutHint hint;
+  hint.addr_tz = shard_addr_tz(s0.data(), static_cast<int>(s0.size()));
+  if (batch > 1) {
+    const int v = t.valid[0];
+    auto addr = [&](int b) { return reinterpret_cast<uintptr_t>(shard_ptr(b, v)); };
+    const uint64_t stride = addr(1) - addr(0);
+    bool regular = true;
+    for (int b = 2; b < batch && regular; ++b) regular = addr(b) - addr(b - 1) == stride;
+    if (regular) hint.stripe_stride = stride;
+  }
+  return hint;
 }
 
 hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_t* d, size_t S,
-                         hipStream_t s, int status_stride, int addr_tz) {
+                         hipStream_t s, int status_stride, const LayoutHint& hint) {
   for (size_t gi = 0; gi < t.groups.size(); ++gi) {
     const Group& g = t.groups[gi];
     ApplyArgs a{};
@@ -299,7 +317,8 @@ hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_
     a.K = t.k;
     a.R = static_cast<int>(g.shard.size());
     a.batch = batch;
-    a.addr_tz = addr_tz;
+    a.addr_tz = hint.addr_tz;
+    a.stripe_stride = hint.stripe_stride;
     hipError_t e = launch_apply(a, s);
     if (e != hipSuccess) return e;
   }
@@ -630,12 +649,12 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     sl.meta_tables = nullptr;  // the staged path refills its tables next time
     std::vector<char> is_out(n, 0);
     for (int i : outs) is_out[i] = 1;
-    const int tz = fill_meta(t, DL, batch, static_cast<uint8_t*>(sl.hmeta.p), [&](int b, int i) {
+    const LayoutHint hint = fill_meta(t, DL, batch, static_cast<uint8_t*>(sl.hmeta.p), [&](int b, int i) {
       return is_out[i] ? static_cast<const uint8_t*>(host_out(b, i)) : host_in(b, i);
     });
     auto* meta = static_cast<uint8_t*>(sl.meta.p);
     HIPCHK(hipMemcpyAsync(meta, sl.hmeta.p, DL.total, hipMemcpyHostToDevice, sl.stream));
-    HIPCHK(launch_groups(t, DL, batch, meta, S, sl.stream, 1, tz));
+    HIPCHK(launch_groups(t, DL, batch, meta, S, sl.stream, 1, hint));
     if (verify)
       HIPCHK(hipMemcpyAsync(sl.hstat.p, meta + DL.status_off, sizeof(int) * batch,
                             hipMemcpyDeviceToHost, sl.stream));
@@ -677,7 +696,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     if (sl.meta_tables != tp || sl.meta_pitch != cpitch || sl.meta_spc != spc ||
         sl.meta_base != sl.dev.p) {
       auto* base = static_cast<uint8_t*>(sl.dev.p);
-      sl.meta_tz = fill_meta(t, ML, spc, static_cast<uint8_t*>(sl.hmeta.p),
+      sl.meta_hint = fill_meta(t, ML, spc, static_cast<uint8_t*>(sl.hmeta.p),
                              [&](int b, int i) { return base + spitch * b + cpitch * i; });
       HIPCHK(hipMemcpyAsync(sl.meta.p, sl.hmeta.p, ML.total, hipMemcpyHostToDevice, sl.stream));
       sl.meta_tables = tp;
@@ -746,7 +765,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
                               sl.stream));
     }
     if (verify) HIPCHK(hipMemsetAsync(dstatus, 0, sizeof(int) * cnt, sl.stream));
-    HIPCHK(launch_groups(t, ML, cnt, meta, w, sl.stream, 1, sl.meta_tz));
+    HIPCHK(launch_groups(t, ML, cnt, meta, w, sl.stream, 1, sl.meta_hint));
     if (!outs.empty()) {
       if (coalesce) {
         const size_t bytes = spitch * (cnt - 1) + cpitch * (out_hi - out_lo) + w;
@@ -1150,7 +1169,7 @@ struct rs_plan {
   MetaLayout layout;
   void* dmeta = nullptr;
   uint64_t bytes = 0;
-  int addr_tz = 0;
+  LayoutHint hint;
 };
 
 int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
@@ -1179,7 +1198,7 @@ int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
   plan->layout = meta_layout(*t, batch);
   plan->bytes = algo_bytes(*t, S, batch);
   std::vector<uint8_t> h(plan->layout.total);
-  plan->addr_tz = fill_meta(*t, plan->layout, batch, h.data(), [&](int b, int i) {
+  plan->hint = fill_meta(*t, plan->layout, batch, h.data(), [&](int b, int i) {
     return static_cast<const uint8_t*>(shards[static_cast<size_t>(b) * n + i]);
   });
   HIPCHK(hipSetDevice(device));
@@ -1197,7 +1216,7 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
   HIPCHK(hipSetDevice(plan->device));
   HIPCHK(launch_groups(*plan->tables, plan->layout, plan->batch,
                        static_cast<uint8_t*>(plan->dmeta), plan->S,
-                       static_cast<hipStream_t>(stream), /*status_stride=*/1, plan->addr_tz));
+                       static_cast<hipStream_t>(stream), /*status_stride=*/1, plan->hint));
   return RS_OK;
 }
 

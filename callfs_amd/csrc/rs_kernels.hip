@@ -67,8 +67,17 @@ using LdsG2Policy = dev::Policy<2, 1, true, true, false, 512, 2, 5>;
 using LdsQ8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 6>;
 using LdsQ16Policy = dev::Policy<2, 1, true, true, false, 512, 2, 8>;
 enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16 };
-TileOrder lds_tile_order(uint64_t S, uint64_t nvec, int addr_tz, int streams) {
+TileOrder lds_tile_order(uint64_t S, uint64_t nvec, int addr_tz, int streams,
+                         uint64_t stripe_stride) {
   const uint64_t tps = (nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;
+  // stripes exactly 2 MiB apart: interleaving stripes costs 2-12 points (RS(8,8) 128 KiB
+  // 72.4 -> 60.6 with G8, RS(4,4) 256 KiB 77.9 -> 65.8, RS(6,2) 256 KiB 81.5 -> 78.4);
+  // strides of 1, 4, 8 or 16 MiB interleave fine (profiles/r01/tile_order/segments/
+  // ord_stride*). Consecutive tiles there.
+  if (stripe_stride == (2ull << 20) && tps <= 1024) return TileOrder::kConsecutive;
+  // exactly 1 MiB apart: G2 beats G8 (RS(4,4) 128 KiB 61.2 -> 68.7, RS(8,8) 64 KiB 64.2
+  // -> 67.7, RS(12,4) 64 KiB equal)
+  if (stripe_stride == (1ull << 20) && tps <= 32) return TileOrder::kGroup2;
   if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
   if (tps <= 128 || (tps <= 1024 && streams >= 14)) return TileOrder::kGroup2;
   if (tps <= 1024) return TileOrder::kConsecutive;  // S <= 8 MiB, few streams
@@ -135,7 +144,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
-          switch (lds_tile_order(a.S, a.nvec, a.addr_tz, a.K + a.R)) {
+          switch (lds_tile_order(a.S, a.nvec, a.addr_tz, a.K + a.R, a.stripe_stride)) {
             case TileOrder::kGroup8: fn = kLdsG8[a.R - 1]; break;
             case TileOrder::kGroup2: fn = kLdsG2[a.R - 1]; break;
             case TileOrder::kSeg8: fn = kLdsQ8[a.R - 1]; break;

@@ -30,6 +30,9 @@ struct ApplyArgs {
   // addresses of a stripe (shard_addr_tz); picks the LDS kernel's tile order. 0 = odd
   // or unknown.
   int addr_tz;
+  // byte distance between consecutive stripes' shards when it is the same for every
+  // stripe (0 = one stripe or irregular); also keys the tile order.
+  uint64_t stripe_stride;
 };
 
 // addr_tz for a set of shard addresses: trailing zeros of the OR of their differences

@@ -337,6 +337,8 @@ def test_plan_misaligned_pointers(native_lib, k, m, S, off):
     (10, 4, (9 << 20) + 3, (9 << 20) + 256, 2),  # few trailing zeros: consecutive tiles
     (16, 4, 700_000, 1 << 20, 3),             # <= 1 MiB: 2-stripe interleave
     (4, 2, (3 << 20) + 9, 4 << 20, 3),        # 1-8 MiB, 6 streams: consecutive
+    (12, 4, 100_000, 1 << 17, 5),             # stripes exactly 2 MiB apart: consecutive
+    (4, 4, 120_000, 1 << 17, 6),              # stripes exactly 1 MiB apart: 2-stripe interleave
     (4, 4, 100_000, 1 << 17, 9),              # <= 256 KiB: 8-stripe interleave, ragged group
     (10, 12, (3 << 20) + 4112, 4 << 20, 2),   # 16-row group >= 2 MiB: 8 column segments
     (10, 16, (1 << 20) + 48, 2 << 20, 1),     # 16-row group < 2 MiB: consecutive

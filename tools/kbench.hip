@@ -107,6 +107,32 @@ __global__ __launch_bounds__(512) void write_stream(ApplyArgs a) {
     dev::store16<P>(reinterpret_cast<uint4*>(out[r]) + v, make_uint4(t, r, 7, 9));
 }
 
+// Read probe: every shard stream of the layout (K inputs and the R output slots) read in
+// tile order ORD, nothing stored unless an impossible value -- a side-effect-free
+// stand-in for the kernel's access pattern (does its ranking of tile orders match the
+// kernel's?).
+template <int ORD>
+__global__ __launch_bounds__(512) void read_probe(ApplyArgs a) {
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + 511) / 512);
+  uint32_t stripe, tile;
+  dev::map_tile<ORD>(blockIdx.x, tps, static_cast<uint32_t>(a.batch), stripe, tile);
+  const uint64_t v = static_cast<uint64_t>(tile) * 512 + threadIdx.x;
+  if (v >= a.nvec) return;
+  using P = dev::Policy<4, 1, true, true, false>;
+  dev::cptr<const uint8_t*> in = dev::as_const(a.in_tab) + static_cast<size_t>(stripe) * a.K;
+  dev::cptr<uint8_t*> out = dev::as_const(a.out_tab) + static_cast<size_t>(stripe) * a.R;
+  uint32_t acc = 0;
+  for (int i = 0; i < a.K; ++i) {
+    const uint4 x = dev::load16<P>(reinterpret_cast<const uint4*>(in[i]) + v);
+    acc ^= x.x ^ x.y ^ x.z ^ x.w;
+  }
+  for (int r = 0; r < a.R; ++r) {
+    const uint4 x = dev::load16<P>(reinterpret_cast<const uint4*>(out[r]) + v);
+    acc ^= x.x ^ x.y ^ x.z ^ x.w;
+  }
+  if (acc == 0x9E3779B9u && v == 12345) *a.status = 1;
+}
+
 struct Variant {
   std::string name;
   std::function<void(const ApplyArgs&, hipStream_t)> launch;
@@ -210,6 +236,7 @@ int main(int argc, char** argv) {
     std::vector<const void*> s0(in.begin(), in.begin() + k);
     s0.insert(s0.end(), out.begin(), out.begin() + m);
     a.addr_tz = shard_addr_tz(s0.data(), k + m);
+    a.stripe_stride = B > 1 ? static_cast<uint64_t>(pitch) * n : 0;
   }
 
   using namespace dev;
@@ -313,6 +340,15 @@ int main(int argc, char** argv) {
       case 16: KB_WORD(16, W0) break;
     }
   }
+  if (std::getenv("KB_PROBE")) {  // read probes in each tile order (bytes: all n streams)
+#define KB_PROBE_V(NAME, ORD)                                                                  \
+  vs.push_back(Variant{NAME, [](const ApplyArgs& a, hipStream_t s) {                           \
+                         const unsigned g = static_cast<unsigned>((a.nvec + 511) / 512 * a.batch); \
+                         hipLaunchKernelGGL((read_probe<ORD>), dim3(g), dim3(512), 0, s, a);  \
+                       }, false});
+    KB_PROBE_V("probe c", 0) KB_PROBE_V("probe g8", 2) KB_PROBE_V("probe g2", 5)
+    KB_PROBE_V("probe q8", 6) KB_PROBE_V("probe q16", 8) KB_PROBE_V("probe q64", 9)
+  }
   if (std::getenv("KB_RING")) {  // unrolled input ring of PD+1 slots (RING = 1)
     using R2 = Policy<2, 1, true, true, false, 512, 2, 0, 1>;
     using R3 = Policy<2, 1, true, true, false, 512, 3, 0, 1>;
@@ -415,7 +451,7 @@ int main(int argc, char** argv) {
           if (!same) std::printf("MISMATCH variant %s stripe %d\n", vs[vi].name.c_str(), b);
         }
       }
-      if (!vs[vi].check) {  // restore parity clobbered by ceiling kernels
+      if (!vs[vi].check && vs[vi].name.rfind("probe", 0) != 0) {  // restore parity clobbered by ceiling kernels
         for (int b = 0; b < B; ++b)
           CK(hipMemcpy(out[b * m], ref + static_cast<size_t>(b) * m * pitch, m * pitch, hipMemcpyDeviceToDevice));
       }
