@@ -433,26 +433,28 @@ void rs_apply_lds(ApplyArgs a) {
   // the launch passes R == RT; kept as a runtime stride so an RT instance can also
   // serve fewer rows (rows >= R are computed and dropped)
   const int R = a.R;
-  const uint32_t tps = static_cast<uint32_t>((a.nvec + BS - 1) / BS);
-  const uint32_t t = blockIdx.x;  // one tile per block (vec_grid)
-  uint32_t stripe, tile;
-  map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
-  const uint64_t v0 = static_cast<uint64_t>(tile) * BS + threadIdx.x;
-  const bool live = t < tps * static_cast<uint32_t>(a.batch) && v0 < a.nvec;
-  cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
-  cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
-  auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.ltabs);
     uint4* dst = reinterpret_cast<uint4*>(smem);
     for (int j = threadIdx.x; j < K * 2 * W; j += BS) dst[j] = src[j];
   }
   __syncthreads();
-  if (!live) return;
   // absolute LDS address of the tables (0 unless static LDS is ever added)
   const uint32_t lds0 = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)smem));
-  {
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + BS - 1) / BS);
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
+  // one tile per block (vec_grid), or (PERSIST) grid-stride over tiles so that the
+  // table prologue is paid once per block; either way the blocks in flight cover a
+  // window of consecutive t, which is what the tile order arranges
+  for (uint32_t t = blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
+    uint32_t stripe, tile;
+    map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
+    const uint64_t v0 = static_cast<uint64_t>(tile) * BS + threadIdx.x;
+    if (v0 >= a.nvec) continue;
+    cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
+    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
+    auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
     AccT acc[4][4];
 #pragma unroll
     for (int w = 0; w < 4; ++w)
