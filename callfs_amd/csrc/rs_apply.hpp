@@ -152,6 +152,34 @@ __device__ __forceinline__ void mac_one(uint32_t (&acc)[U][RT][4], const uint4 (
     }
 }
 
+// Block t -> (stripe, column tile) for tile order ORD (Policy::ORD; LDS kernel and the
+// tools/kbench read probe). tps = tiles per stripe; t < tps * batch.
+template <int ORD>
+__device__ __forceinline__ void map_tile(uint32_t t, uint32_t tps, uint32_t batch,
+                                         uint32_t& stripe, uint32_t& tile) {
+  if constexpr (ORD == 0) {
+    stripe = t / tps;
+    tile = t - stripe * tps;
+  } else if constexpr (ORD >= 6) {
+    // one stripe at a time, its columns cut into Q segments; neighbouring blocks take
+    // the same position of different segments (tiles past the last full round of Q
+    // keep their place, so the map stays a bijection)
+    constexpr uint32_t Q = ORD == 6 ? 8 : (ORD == 7 ? 32 : (ORD == 8 ? 16 : 64));
+    stripe = t / tps;
+    const uint32_t r = t - stripe * tps, seg = tps / Q;
+    tile = r < seg * Q ? (r % Q) * seg + r / Q : r;
+  } else {
+    // groups of G stripes whose tiles interleave (neighbouring blocks: same offset of
+    // different stripes)
+    constexpr uint32_t G = ORD == 2 ? 8 : (ORD == 3 ? 32 : (ORD == 4 ? 4 : 2));
+    const uint32_t per_group = G * tps;
+    const uint32_t g = t / per_group, r = t - g * per_group;
+    const uint32_t gsz = std::min<uint32_t>(G, batch - g * G);
+    tile = r / gsz;
+    stripe = g * G + (r - tile * gsz);
+  }
+}
+
 // Tiles: a stripe's nvec vectors are cut into tiles of BS*U; tile t covers stripe
 // t / tiles_per_stripe (ORD 0) or t % batch (ORD 1). Every tile is wave-uniform in its
 // stripe, so shard pointers stay scalar.
@@ -169,20 +197,11 @@ void rs_apply_vec(ApplyArgs a) {
 
   for (uint32_t t = blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
     uint32_t stripe, tile;
-    if constexpr (P::ORD == 0) {
-      stripe = t / tps;
-      tile = t - stripe * tps;
-    } else if constexpr (P::ORD == 1) {
+    if constexpr (P::ORD == 1) {
       tile = t / static_cast<uint32_t>(a.batch);
       stripe = t - tile * static_cast<uint32_t>(a.batch);
     } else {
-      // groups of G stripes, tiles interleaved across the group's stripes
-      constexpr uint32_t G = P::ORD == 2 ? 8 : 32;
-      const uint32_t per_group = G * tps;
-      const uint32_t g = t / per_group, r = t - g * per_group;
-      const uint32_t gsz = std::min<uint32_t>(G, static_cast<uint32_t>(a.batch) - g * G);
-      tile = r / gsz;
-      stripe = g * G + (r - tile * gsz);
+      map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
     }
     const uint64_t v0 = static_cast<uint64_t>(tile) * tile_vecs + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
@@ -263,34 +282,6 @@ void rs_apply_vec(ApplyArgs a) {
       }
     }
     if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
-  }
-}
-
-// Block t -> (stripe, column tile) for tile order ORD (Policy::ORD; LDS kernel and the
-// tools/kbench read probe). tps = tiles per stripe; t < tps * batch.
-template <int ORD>
-__device__ __forceinline__ void map_tile(uint32_t t, uint32_t tps, uint32_t batch,
-                                         uint32_t& stripe, uint32_t& tile) {
-  if constexpr (ORD == 0) {
-    stripe = t / tps;
-    tile = t - stripe * tps;
-  } else if constexpr (ORD >= 6) {
-    // one stripe at a time, its columns cut into Q segments; neighbouring blocks take
-    // the same position of different segments (tiles past the last full round of Q
-    // keep their place, so the map stays a bijection)
-    constexpr uint32_t Q = ORD == 6 ? 8 : (ORD == 7 ? 32 : (ORD == 8 ? 16 : 64));
-    stripe = t / tps;
-    const uint32_t r = t - stripe * tps, seg = tps / Q;
-    tile = r < seg * Q ? (r % Q) * seg + r / Q : r;
-  } else {
-    // groups of G stripes whose tiles interleave (neighbouring blocks: same offset of
-    // different stripes)
-    constexpr uint32_t G = ORD == 2 ? 8 : (ORD == 3 ? 32 : (ORD == 4 ? 4 : 2));
-    const uint32_t per_group = G * tps;
-    const uint32_t g = t / per_group, r = t - g * per_group;
-    const uint32_t gsz = std::min<uint32_t>(G, batch - g * G);
-    tile = r / gsz;
-    stripe = g * G + (r - tile * gsz);
   }
 }
 

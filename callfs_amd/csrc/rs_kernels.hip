@@ -21,6 +21,14 @@ using dev::kBlock;
 // 8 TB/s) vs 5457 GB/s for the first compile-time-K / plain-load version and
 // 5957 GB/s for an XOR-only kernel with the same loads and stores. Used for k <= 3.
 using ProdPolicy = dev::Policy<4, 1, true, true, false, 512, 2, 0>;
+// Tile order of the v_perm kernel (k <= 3: at most 7 shard streams per stripe;
+// tools/order_sweep.sh KB_ORD "vperm ord", 7 rounds, % of 8 TB/s,
+// profiles/r01/tile_order/segments/ord_vperm): 2-stripe interleave up to 8 MiB shards
+// (RS(3,2) 1 MiB 74.9 -> 77.6, 5.6 MB 75.6 -> 80.6, RS(2,1) 64 KiB 74.9 -> 78.2, RS(2,2)
+// 4 MiB 75.9 -> 77.6; RS(1,1) 1 MiB 79.2 -> 78.4), 16 column segments above 8 MiB when
+// the shards sit at multiples of 8 MiB (RS(3,2) 16 MiB 72.7 -> 77.7), else consecutive.
+using ProdG2Policy = dev::Policy<4, 1, true, true, false, 512, 2, 5>;
+using ProdQ16Policy = dev::Policy<4, 1, true, true, false, 512, 2, 8>;
 
 // The LDS nibble-table kernel takes every launch with k >= 4 inputs or R >= 5 rows. Its
 // cost per data byte barely grows with R, and with all 8 lookups of a dword in flight it
@@ -116,6 +124,12 @@ constexpr auto byte_table(std::integer_sequence<int, Rs...>) {
 }
 
 const auto kVec = vec_table(std::make_integer_sequence<int, kPermMaxRows>{});
+template <class P, int... Rs>
+constexpr auto vec_order_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_vec<0, Rs + 1, P>...};
+}
+const auto kVecG2 = vec_order_table<ProdG2Policy>(std::make_integer_sequence<int, 4>{});
+const auto kVecQ16 = vec_order_table<ProdQ16Policy>(std::make_integer_sequence<int, 4>{});
 const auto kLds = lds_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 const auto kLdsG8 = lds_order_table<LdsG8Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsG2 = lds_order_table<LdsG2Policy>(std::make_integer_sequence<int, 8>{});
@@ -171,8 +185,15 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         const unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         hipLaunchKernelGGL(fn, dim3(gx), dim3(LdsPolicy::BS), lds, stream, a);
       } else {
+        VecFn fn = kVec[a.R - 1];  // R <= 4 here (R >= kLdsMinRows takes the LDS kernel)
+        const uint64_t tps = (a.nvec + ProdPolicy::BS - 1) / ProdPolicy::BS;
+        if (tps <= 1024) fn = kVecG2[a.R - 1];
+        else if (a.addr_tz >= 23 && a.S < (128ull << 20)) fn = kVecQ16[a.R - 1];
+        static_assert(ProdG2Policy::BS == ProdPolicy::BS && ProdQ16Policy::BS == ProdPolicy::BS &&
+                          ProdG2Policy::U == ProdPolicy::U && ProdQ16Policy::U == ProdPolicy::U,
+                      "one grid shape for every v_perm policy");
         const unsigned gx = dev::vec_grid<ProdPolicy>(a.nvec, a.batch);
-        hipLaunchKernelGGL(kVec[a.R - 1], dim3(gx), dim3(ProdPolicy::BS), 0, stream, a);
+        hipLaunchKernelGGL(fn, dim3(gx), dim3(ProdPolicy::BS), 0, stream, a);
       }
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;

@@ -339,6 +339,8 @@ def test_plan_misaligned_pointers(native_lib, k, m, S, off):
     (4, 2, (3 << 20) + 9, 4 << 20, 3),        # 1-8 MiB, 6 streams: consecutive
     (12, 4, 100_000, 1 << 17, 5),             # stripes exactly 2 MiB apart: consecutive
     (4, 4, 120_000, 1 << 17, 6),              # stripes exactly 1 MiB apart: 2-stripe interleave
+    (3, 2, (12 << 20) + 100, 16 << 20, 2),    # v_perm kernel (k <= 3), 16 column segments
+    (2, 3, 300_001, 300_032, 5),              # v_perm kernel, 2-stripe interleave, odd batch
     (4, 4, 100_000, 1 << 17, 9),              # <= 256 KiB: 8-stripe interleave, ragged group
     (10, 12, (3 << 20) + 4112, 4 << 20, 2),   # 16-row group >= 2 MiB: 8 column segments
     (10, 16, (1 << 20) + 48, 2 << 20, 1),     # 16-row group < 2 MiB: consecutive

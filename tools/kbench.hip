@@ -298,6 +298,20 @@ int main(int argc, char** argv) {
         launch_lds<1, L512w2>, launch_lds<2, L512w2>, launch_lds<3, L512w2>, launch_lds<4, L512w2>};
     vs.push_back(Variant{"lds prod-policy", [m](const ApplyArgs& a, hipStream_t s) { lds_r[m - 1](a, s); }});
   }
+  if (k <= 3 && m <= 4 && std::getenv("KB_ORD")) {  // v_perm kernel tile orders (k <= 3)
+#define KB_VORD(RT)                                                                                       \
+  vs.push_back(make_variant<0, RT, Policy<4, 1, true, true, false, 512, 2, 0>>("vperm ord consec"));   \
+  vs.push_back(make_variant<0, RT, Policy<4, 1, true, true, false, 512, 2, 2>>("vperm ord g8"));       \
+  vs.push_back(make_variant<0, RT, Policy<4, 1, true, true, false, 512, 2, 5>>("vperm ord g2"));       \
+  vs.push_back(make_variant<0, RT, Policy<4, 1, true, true, false, 512, 2, 6>>("vperm ord q8"));       \
+  vs.push_back(make_variant<0, RT, Policy<4, 1, true, true, false, 512, 2, 8>>("vperm ord q16"));
+    switch (m) {
+      case 1: KB_VORD(1) break;
+      case 2: KB_VORD(2) break;
+      case 3: KB_VORD(3) break;
+      case 4: KB_VORD(4) break;
+    }
+  }
   if ((m == 2 || m == 3 || m == 4 || m == 8) && std::getenv("KB_ORD")) {  // LDS kernel tile orders
     using O0 = Policy<2, 1, true, true, false, 512, 2, 0>;
     using O2 = Policy<2, 1, true, true, false, 512, 2, 2>;
