@@ -627,7 +627,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   // write the caller's bytes over PCIe in one launch set over the whole call -- no
   // staging copies, no chunk pipeline, nothing for the CPU but the join of present
   // data shards. RS(10,4) 64 MiB: 43.7 GiB/s vs 36.7 for H2D + launch + D2H
-  // (tools/zerocopy_probe.py).
+  // (tests/perf/zerocopy_probe.py).
   static const unsigned long long zc_min = [] {
     const char* e = std::getenv("CALLFS_RS_ZERO_COPY_MIN_BYTES");
     return e ? std::strtoull(e, nullptr, 0) : (128ull << 10);  // crossover: 80-160 KiB

@@ -7,9 +7,9 @@
  * the object size above which the shim should hand a request to the GPU (INTEGRATION.md,
  * CALLFS_ERASURE__GPU_MIN_BYTES).
  *
- * build: gcc -O2 tools/cpu_port_native.c -Loracle/build -lrs_oracle \
- *          -Wl,-rpath,'$ORIGIN/../oracle/build' -o tools/cpu_port_native
- * run:   tools/cpu_port_native k m object_bytes threads seconds
+ * build: gcc -O2 tests/perf/cpu_port_native.c -Loracle/build -lrs_oracle \
+ *          -Wl,-rpath,'$ORIGIN/../../oracle/build' -o tests/perf/cpu_port_native
+ * run:   tests/perf/cpu_port_native k m object_bytes threads seconds
  */
 #include <stdint.h>
 #include <stdio.h>

@@ -7,7 +7,7 @@ data shards aliasing the object as upstream Split does. Paired with
 object size above which the shim should hand a request to the GPU
 (INTEGRATION.md, CALLFS_ERASURE__GPU_MIN_BYTES).
 
-usage: python tools/cpu_port_sweep.py [--k 10 --m 4 --threads 1,16 --sizes 64K,1M,...]
+usage: python tests/perf/cpu_port_sweep.py [--k 10 --m 4 --threads 1,16 --sizes 64K,1M,...]
 """
 import argparse
 import json
@@ -15,7 +15,7 @@ import os
 import sys
 import time
 
-HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, HERE)
 
 import numpy as np  # noqa: E402

@@ -7,14 +7,14 @@ launch over host shards (inputs read by the kernel over PCIe, parity written bac
 PCIe) against H2D + launch + D2H through device buffers, and checks the bytes against
 the CPU oracle.
 
-usage: python tools/zerocopy_probe.py [--k 10 --m 4 --object-bytes 67108864]
+usage: python tests/perf/zerocopy_probe.py [--k 10 --m 4 --object-bytes 67108864]
 """
 import argparse
 import json
 import os
 import sys
 
-HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, HERE)
 
 import numpy as np  # noqa: E402

@@ -11,6 +11,6 @@ for L in 1048576 16777216 67108864 268435456; do
     echo "{\"mode\": \"pinned\", \"threads\": $th}" >> $O
     CALLFS_E2E_PINNED=1 CALLFS_E2E_ENCODER=1 timeout -k 10 60 tools/e2e_native 4 2 $L $th 1.0 1,4 >> $O || exit 1
   done
-  for th in 1 16; do timeout -k 10 30 tools/cpu_port_native 4 2 $L $th 1.0 >> $O || exit 1; done
+  for th in 1 16; do timeout -k 10 30 tests/perf/cpu_port_native 4 2 $L $th 1.0 >> $O || exit 1; done
 done
 echo ok
