@@ -53,10 +53,10 @@ __device__ __forceinline__ void compress(uint32_t (&st)[8], uint32_t (&w)[16]) {
       w[t & 15] = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
     }
     const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);  // e ? f : g
     const uint32_t t1 = h + S1 + ch + kK[t] + w[t & 15];
     const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-    const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t maj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);  // majority
     h = g;
     g = f;
     f = e;
