@@ -376,6 +376,38 @@ def test_plan_tile_orders_vs_oracle(native_lib, k, m, S, pitch, batch):
     assert np.array_equal(view.cpu().numpy(), want_all)
 
 
+def test_full_size_bench_shape_linearity_and_matrix(native_lib):
+    """The bench workload at full size (RS(10,4), 1 MiB shards, 256 stripes) through
+    size-independent properties, compared on the device: encode is GF(2)-linear
+    (parity(A ^ B) == parity(A) ^ parity(B)), and a stripe whose only nonzero data is
+    byte value v in shard i has parity row j equal to mul(P[j][i], v) at every byte, with
+    P from the oracle's encode matrix (pinned by the upstream known-answer values)."""
+    import torch
+    from callfs_amd.device import Plan
+    k, m, S, batch = 10, 4, 1 << 20, 256
+    a = _batch(k, m, S, batch, seed=101)
+    b = _batch(k, m, S, batch, seed=202)
+    c = _batch(k, m, S, batch, seed=303)
+    c.buf[:, :k] = a.buf[:, :k] ^ b.buf[:, :k]
+    for sb in (a, b, c):
+        Plan.for_batch(sb).launch()
+    torch.cuda.synchronize()
+    assert torch.equal(c.parity(), a.parity() ^ b.parity())
+    del b, c
+    # impulses: stripe s carries value v = s + 1 in data shard s % k, zeros elsewhere
+    a.buf.zero_()
+    vals = torch.arange(1, batch + 1, dtype=torch.int64) % 256
+    for s in range(batch):
+        a.buf[s, s % k, :S] = int(vals[s])
+    Plan.for_batch(a).launch()
+    torch.cuda.synchronize()
+    P = cref.encode_matrix(k, m)[k:]
+    want = torch.tensor([[o.gal_mul(int(P[j][s % k]), int(vals[s])) for j in range(m)]
+                         for s in range(batch)], dtype=torch.uint8, device=a.buf.device)
+    par = a.parity()
+    assert torch.equal(par.amin(dim=2), want) and torch.equal(par.amax(dim=2), want)
+
+
 def test_full_size_config_rs10_4_64mib_roundtrip(native_lib):
     """configs[1]/[2] at full size: 256 objects of 64 MiB (S = 6,710,887; 22.4 GiB of
     shards in HBM). Encode the batch, erase 4 shards per pattern, decode, require every
