@@ -3,7 +3,9 @@
 // on MI355X (DESIGN.md "Kernel tuning log").
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <mutex>
+#include <string>
 #include <type_traits>
 #include <utility>
 
@@ -96,6 +98,22 @@ TileOrder lds_tile_order(uint64_t S, uint64_t nvec, int addr_tz, int streams,
   }
   return TileOrder::kConsecutive;
 }
+// CALLFS_RS_TILE_ORDER=consecutive|g8|g2|q8|q16 overrides the rule for every LDS-kernel
+// launch with R <= 8 (A/B on a deployment's own shard layout; unset = the rule).
+int tile_order_override() {
+  static const int v = [] {
+    const char* e = std::getenv("CALLFS_RS_TILE_ORDER");
+    if (!e) return -1;
+    const std::string o(e);
+    if (o == "consecutive") return static_cast<int>(TileOrder::kConsecutive);
+    if (o == "g8") return static_cast<int>(TileOrder::kGroup8);
+    if (o == "g2") return static_cast<int>(TileOrder::kGroup2);
+    if (o == "q8") return static_cast<int>(TileOrder::kSeg8);
+    if (o == "q16") return static_cast<int>(TileOrder::kSeg16);
+    return -1;
+  }();
+  return v;
+}
 constexpr int kLdsMinRows = 5;
 constexpr int kLdsMinK = 4;
 constexpr int kPermMaxRows = 8;  // v_perm kernel instantiations (production: k <= 3, R <= 4)
@@ -158,7 +176,9 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
-          switch (lds_tile_order(a.S, a.nvec, a.addr_tz, a.K + a.R, a.stripe_stride)) {
+          const int forced = tile_order_override();
+          switch (forced >= 0 ? static_cast<TileOrder>(forced)
+                              : lds_tile_order(a.S, a.nvec, a.addr_tz, a.K + a.R, a.stripe_stride)) {
             case TileOrder::kGroup8: fn = kLdsG8[a.R - 1]; break;
             case TileOrder::kGroup2: fn = kLdsG2[a.R - 1]; break;
             case TileOrder::kSeg8: fn = kLdsQ8[a.R - 1]; break;
