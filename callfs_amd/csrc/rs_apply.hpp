@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "rs_kernels.hpp"
+#include "tile_order.hpp"
 
 namespace callfs {
 namespace dev {
@@ -150,34 +151,6 @@ __device__ __forceinline__ void mac_one(uint32_t (&acc)[U][RT][4], const uint4 (
 #pragma unroll
       for (int r = 0; r < RT; ++r) acc[u][r][w] = fma1(acc[u][r][w], gf_mul4(sa, ta + r * 5));
     }
-}
-
-// Block t -> (stripe, column tile) for tile order ORD (Policy::ORD; LDS kernel and the
-// tools/kbench read probe). tps = tiles per stripe; t < tps * batch.
-template <int ORD>
-__device__ __forceinline__ void map_tile(uint32_t t, uint32_t tps, uint32_t batch,
-                                         uint32_t& stripe, uint32_t& tile) {
-  if constexpr (ORD == 0) {
-    stripe = t / tps;
-    tile = t - stripe * tps;
-  } else if constexpr (ORD >= 6) {
-    // one stripe at a time, its columns cut into Q segments; neighbouring blocks take
-    // the same position of different segments (tiles past the last full round of Q
-    // keep their place, so the map stays a bijection)
-    constexpr uint32_t Q = ORD == 6 ? 8 : (ORD == 7 ? 32 : (ORD == 8 ? 16 : 64));
-    stripe = t / tps;
-    const uint32_t r = t - stripe * tps, seg = tps / Q;
-    tile = r < seg * Q ? (r % Q) * seg + r / Q : r;
-  } else {
-    // groups of G stripes whose tiles interleave (neighbouring blocks: same offset of
-    // different stripes)
-    constexpr uint32_t G = ORD == 2 ? 8 : (ORD == 3 ? 32 : (ORD == 4 ? 4 : 2));
-    const uint32_t per_group = G * tps;
-    const uint32_t g = t / per_group, r = t - g * per_group;
-    const uint32_t gsz = std::min<uint32_t>(G, batch - g * G);
-    tile = r / gsz;
-    stripe = g * G + (r - tile * gsz);
-  }
 }
 
 // Tiles: a stripe's nvec vectors are cut into tiles of BS*U; tile t covers stripe

@@ -10,6 +10,7 @@
 #include <utility>
 
 #include "rs_apply.hpp"
+#include "tile_order.hpp"
 
 namespace callfs {
 
@@ -23,12 +24,6 @@ using dev::kBlock;
 // 8 TB/s) vs 5457 GB/s for the first compile-time-K / plain-load version and
 // 5957 GB/s for an XOR-only kernel with the same loads and stores. Used for k <= 3.
 using ProdPolicy = dev::Policy<4, 1, true, true, false, 512, 2, 0>;
-// Tile order of the v_perm kernel (k <= 3: at most 7 shard streams per stripe;
-// tools/order_sweep.sh KB_ORD "vperm ord", 7 rounds, % of 8 TB/s,
-// profiles/r01/tile_order/segments/ord_vperm): 2-stripe interleave up to 8 MiB shards
-// (RS(3,2) 1 MiB 74.9 -> 77.6, 5.6 MB 75.6 -> 80.6, RS(2,1) 64 KiB 74.9 -> 78.2, RS(2,2)
-// 4 MiB 75.9 -> 77.6; RS(1,1) 1 MiB 79.2 -> 78.4), 16 column segments above 8 MiB when
-// the shards sit at multiples of 8 MiB (RS(3,2) 16 MiB 72.7 -> 77.7), else consecutive.
 using ProdG2Policy = dev::Policy<4, 1, true, true, false, 512, 2, 5>;
 using ProdQ16Policy = dev::Policy<4, 1, true, true, false, 512, 2, 8>;
 
@@ -46,58 +41,13 @@ using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
 // 60.7 % of 8 TB/s (tools/kbench.hip, KB_RING). For R <= 8 the unrolled ring measured
 // 1-3 % slower than the shifted ring of three, so those keep LdsPolicy.
 using LdsWidePolicy = dev::Policy<2, 1, true, true, false, 512, 4, 0, 1>;
-// Wide groups hold 19-32 shard streams per stripe; from 2 MiB shards on, 8 interleaved
-// column segments beat consecutive tiles (tools/order_sweep.sh, KB_ORD, 9 rounds, % of
-// 8 TB/s: RS(10,12) 4 MiB 60.3 -> 66.9, RS(10,16) 16 MiB 58.0 -> 66.7; at 1 MiB all
-// orders are within 0.6 of each other, profiles/r01/tile_order/segments/ord_wide).
 using LdsWideQ8Policy = dev::Policy<2, 1, true, true, false, 512, 4, 6, 1>;
-constexpr uint64_t kWideSegMinTiles = 256;  // S >= 2 MiB
 template <int R>
 using LdsPolicyFor = typename std::conditional<(R > 8), LdsWidePolicy, LdsPolicy>::type;
-// Tile order for R <= 8 (Policy::ORD; tools/kbench.hip KB_ORD, tools/order_sweep.sh,
-// 5-15 rounds, % of 8 TB/s, DESIGN.md "Tile order"). Neighbouring blocks normally take
-// neighbouring column tiles of one stripe (consecutive). For small shards it pays to
-// interleave the same column tile of G stripes instead: G8 up to 256 KiB (RS(10,4)
-// 256 KiB 70.8 -> 73.3-74.0, RS(16,4) 64 KiB 70.9 -> 73.5), G2 up to 1 MiB (512 KiB
-// 72.6 -> 77.6, RS(6,3) 1 MiB 73.7 -> 79.3, RS(10,4) 1 MiB 78.8 -> 79.7) and, for 14 or
-// more shard streams per stripe, up to 8 MiB (RS(16,4) 4 MiB 69.5 -> 75.2, 64 MiB
-// objects 74.6 -> 76.5); with fewer streams G2 loses 1-3.5 points at 4 MiB (RS(4,2)
-// 79.1 -> 75.6), so those keep consecutive tiles. Above 8 MiB, shards whose addresses
-// differ by multiples of 8 MiB (addr_tz >= 23: power-of-two pitches, 24/48 MiB) lose
-// 5-13 points in consecutive order once a stripe has 12 or more streams; interleaving
-// Q column segments of the stripe recovers it: Q16 for 16-32 MiB (RS(10,4) 16 MiB 67.6
-// -> 75.6, RS(16,4) 16 MiB 64.4 -> 77.6, RS(8,4) 32 MiB 71.5 -> 80.1), Q8 otherwise
-// below 128 MiB (24 MiB 70.9 -> 75.8, 48 MiB 68.9 -> 75.1, 64 MiB 69.3 -> 77.2). With
-// fewer streams Q16 hurts at 16 MiB (RS(4,2) 75.7 -> 67.9), so 6-11 streams keep
-// consecutive tiles up to 16 MiB and take Q8 above (RS(6,3) 32 MiB 75.1 -> 79.0).
-// Pitches with few trailing zeros (the 13-107 MB column slices of 1 GiB objects) and
-// >= 128 MiB keep consecutive tiles.
 using LdsG8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 2>;
 using LdsG2Policy = dev::Policy<2, 1, true, true, false, 512, 2, 5>;
 using LdsQ8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 6>;
 using LdsQ16Policy = dev::Policy<2, 1, true, true, false, 512, 2, 8>;
-enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16 };
-TileOrder lds_tile_order(uint64_t S, uint64_t nvec, int addr_tz, int streams,
-                         uint64_t stripe_stride) {
-  const uint64_t tps = (nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;
-  // stripes exactly 2 MiB apart: interleaving stripes costs 2-12 points (RS(8,8) 128 KiB
-  // 72.4 -> 60.6 with G8, RS(4,4) 256 KiB 77.9 -> 65.8, RS(6,2) 256 KiB 81.5 -> 78.4);
-  // strides of 1, 4, 8 or 16 MiB interleave fine (profiles/r01/tile_order/segments/
-  // ord_stride*). Consecutive tiles there.
-  if (stripe_stride == (2ull << 20) && tps <= 1024) return TileOrder::kConsecutive;
-  // exactly 1 MiB apart: G2 beats G8 (RS(4,4) 128 KiB 61.2 -> 68.7, RS(8,8) 64 KiB 64.2
-  // -> 67.7, RS(12,4) 64 KiB equal)
-  if (stripe_stride == (1ull << 20) && tps <= 32) return TileOrder::kGroup2;
-  if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
-  if (tps <= 128 || (tps <= 1024 && streams >= 14)) return TileOrder::kGroup2;
-  if (tps <= 1024) return TileOrder::kConsecutive;  // S <= 8 MiB, few streams
-  if (addr_tz >= 23 && S < (128ull << 20)) {
-    if (streams >= 12)
-      return addr_tz >= 24 && S <= (32ull << 20) ? TileOrder::kSeg16 : TileOrder::kSeg8;
-    return S <= (16ull << 20) ? TileOrder::kConsecutive : TileOrder::kSeg8;
-  }
-  return TileOrder::kConsecutive;
-}
 // CALLFS_RS_TILE_ORDER=consecutive|g8|g2|q8|q16 overrides the rule for every LDS-kernel
 // launch with R <= 8 (A/B on a deployment's own shard layout; unset = the rule).
 int tile_order_override() {
@@ -178,14 +128,16 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
           const int forced = tile_order_override();
           switch (forced >= 0 ? static_cast<TileOrder>(forced)
-                              : lds_tile_order(a.S, a.nvec, a.addr_tz, a.K + a.R, a.stripe_stride)) {
+                              : lds_tile_order(a.S, (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS,
+                                               a.addr_tz, a.K + a.R, a.stripe_stride)) {
             case TileOrder::kGroup8: fn = kLdsG8[a.R - 1]; break;
             case TileOrder::kGroup2: fn = kLdsG2[a.R - 1]; break;
             case TileOrder::kSeg8: fn = kLdsQ8[a.R - 1]; break;
             case TileOrder::kSeg16: fn = kLdsQ16[a.R - 1]; break;
             case TileOrder::kConsecutive: break;
           }
-        } else if ((a.nvec + LdsWidePolicy::BS - 1) / LdsWidePolicy::BS >= kWideSegMinTiles) {
+        } else if (wide_tile_order((a.nvec + LdsWidePolicy::BS - 1) / LdsWidePolicy::BS) ==
+                   TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }
         if (lds > (64u << 10)) {  // wide groups with many shards: opt in once per kernel
@@ -207,8 +159,11 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
       } else {
         VecFn fn = kVec[a.R - 1];  // R <= 4 here (R >= kLdsMinRows takes the LDS kernel)
         const uint64_t tps = (a.nvec + ProdPolicy::BS - 1) / ProdPolicy::BS;
-        if (tps <= 1024) fn = kVecG2[a.R - 1];
-        else if (a.addr_tz >= 23 && a.S < (128ull << 20)) fn = kVecQ16[a.R - 1];
+        switch (vec_tile_order(a.S, tps, a.addr_tz)) {
+          case TileOrder::kGroup2: fn = kVecG2[a.R - 1]; break;
+          case TileOrder::kSeg16: fn = kVecQ16[a.R - 1]; break;
+          default: break;
+        }
         static_assert(ProdG2Policy::BS == ProdPolicy::BS && ProdQ16Policy::BS == ProdPolicy::BS &&
                           ProdG2Policy::U == ProdPolicy::U && ProdQ16Policy::U == ProdPolicy::U,
                       "one grid shape for every v_perm policy");

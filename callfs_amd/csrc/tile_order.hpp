@@ -1,0 +1,112 @@
+// Tile order of the RS kernels (DESIGN.md §5 "Tile order"): which column tile of which
+// stripe block t works on (map_tile, host and device), and the measured rules that pick
+// the order for a launch (lds_tile_order, wide_tile_order, vec_tile_order; host).
+// Plain C++ apart from the __host__ __device__ marker, so tests/native/host_test.cpp
+// builds it with g++ and checks that every order is a bijection and the rules' choices.
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define CALLFS_HD __host__ __device__
+#else
+#define CALLFS_HD
+#endif
+
+namespace callfs {
+
+// Block t -> (stripe, column tile) for tile order ORD (Policy::ORD; LDS kernel and the
+// tools/kbench read probe). tps = tiles per stripe; t < tps * batch.
+template <int ORD>
+CALLFS_HD inline void map_tile(uint32_t t, uint32_t tps, uint32_t batch, uint32_t& stripe,
+                               uint32_t& tile) {
+  if constexpr (ORD == 0) {
+    stripe = t / tps;
+    tile = t - stripe * tps;
+  } else if constexpr (ORD >= 6) {
+    // one stripe at a time, its columns cut into Q segments; neighbouring blocks take
+    // the same position of different segments (tiles past the last full round of Q
+    // keep their place, so the map stays a bijection)
+    constexpr uint32_t Q = ORD == 6 ? 8 : (ORD == 7 ? 32 : (ORD == 8 ? 16 : 64));
+    stripe = t / tps;
+    const uint32_t r = t - stripe * tps, seg = tps / Q;
+    tile = r < seg * Q ? (r % Q) * seg + r / Q : r;
+  } else {
+    // groups of G stripes whose tiles interleave (neighbouring blocks: same offset of
+    // different stripes)
+    constexpr uint32_t G = ORD == 2 ? 8 : (ORD == 3 ? 32 : (ORD == 4 ? 4 : 2));
+    const uint32_t per_group = G * tps;
+    const uint32_t g = t / per_group, r = t - g * per_group;
+    const uint32_t gsz = std::min<uint32_t>(G, batch - g * G);
+    tile = r / gsz;
+    stripe = g * G + (r - tile * gsz);
+  }
+}
+
+// Launch-time choice; Policy::ORD of each: consecutive 0, G8 2, G2 5, Q8 6, Q16 8.
+enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16 };
+
+// Tile order for R <= 8 (Policy::ORD; tools/kbench.hip KB_ORD, tools/order_sweep.sh,
+// 5-15 rounds, % of 8 TB/s, DESIGN.md "Tile order"). Neighbouring blocks normally take
+// neighbouring column tiles of one stripe (consecutive). For small shards it pays to
+// interleave the same column tile of G stripes instead: G8 up to 256 KiB (RS(10,4)
+// 256 KiB 70.8 -> 73.3-74.0, RS(16,4) 64 KiB 70.9 -> 73.5), G2 up to 1 MiB (512 KiB
+// 72.6 -> 77.6, RS(6,3) 1 MiB 73.7 -> 79.3, RS(10,4) 1 MiB 78.8 -> 79.7) and, for 14 or
+// more shard streams per stripe, up to 8 MiB (RS(16,4) 4 MiB 69.5 -> 75.2, 64 MiB
+// objects 74.6 -> 76.5); with fewer streams G2 loses 1-3.5 points at 4 MiB (RS(4,2)
+// 79.1 -> 75.6), so those keep consecutive tiles. Above 8 MiB, shards whose addresses
+// differ by multiples of 8 MiB (addr_tz >= 23: power-of-two pitches, 24/48 MiB) lose
+// 5-13 points in consecutive order once a stripe has 12 or more streams; interleaving
+// Q column segments of the stripe recovers it: Q16 for 16-32 MiB (RS(10,4) 16 MiB 67.6
+// -> 75.6, RS(16,4) 16 MiB 64.4 -> 77.6, RS(8,4) 32 MiB 71.5 -> 80.1), Q8 otherwise
+// below 128 MiB (24 MiB 70.9 -> 75.8, 48 MiB 68.9 -> 75.1, 64 MiB 69.3 -> 77.2). With
+// fewer streams Q16 hurts at 16 MiB (RS(4,2) 75.7 -> 67.9), so 6-11 streams keep
+// consecutive tiles up to 16 MiB and take Q8 above (RS(6,3) 32 MiB 75.1 -> 79.0).
+// Pitches with few trailing zeros (the 13-107 MB column slices of 1 GiB objects) and
+// >= 128 MiB keep consecutive tiles.
+//
+// tps = tiles of 512 16-B vectors (8 KiB) per stripe; streams = K + R of the launch;
+// addr_tz / stripe_stride as in ApplyArgs.
+inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int streams,
+                                uint64_t stripe_stride) {
+  // stripes exactly 2 MiB apart: interleaving stripes costs 2-12 points (RS(8,8) 128 KiB
+  // 72.4 -> 60.6 with G8, RS(4,4) 256 KiB 77.9 -> 65.8, RS(6,2) 256 KiB 81.5 -> 78.4);
+  // strides of 1, 4, 8 or 16 MiB interleave fine (profiles/r01/tile_order/segments/
+  // ord_stride*). Consecutive tiles there.
+  if (stripe_stride == (2ull << 20) && tps <= 1024) return TileOrder::kConsecutive;
+  // exactly 1 MiB apart: G2 beats G8 (RS(4,4) 128 KiB 61.2 -> 68.7, RS(8,8) 64 KiB 64.2
+  // -> 67.7, RS(12,4) 64 KiB equal)
+  if (stripe_stride == (1ull << 20) && tps <= 32) return TileOrder::kGroup2;
+  if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
+  if (tps <= 128 || (tps <= 1024 && streams >= 14)) return TileOrder::kGroup2;
+  if (tps <= 1024) return TileOrder::kConsecutive;  // S <= 8 MiB, few streams
+  if (addr_tz >= 23 && S < (128ull << 20)) {
+    if (streams >= 12)
+      return addr_tz >= 24 && S <= (32ull << 20) ? TileOrder::kSeg16 : TileOrder::kSeg8;
+    return S <= (16ull << 20) ? TileOrder::kConsecutive : TileOrder::kSeg8;
+  }
+  return TileOrder::kConsecutive;
+}
+
+// Wide groups hold 19-32 shard streams per stripe; from 2 MiB shards on, 8 interleaved
+// column segments beat consecutive tiles (tools/order_sweep.sh, KB_ORD, 9 rounds, % of
+// 8 TB/s: RS(10,12) 4 MiB 60.3 -> 66.9, RS(10,16) 16 MiB 58.0 -> 66.7; at 1 MiB all
+// orders are within 0.6 of each other, profiles/r01/tile_order/segments/ord_wide).
+inline TileOrder wide_tile_order(uint64_t tps) {
+  return tps >= 256 ? TileOrder::kSeg8 : TileOrder::kConsecutive;  // S >= 2 MiB
+}
+
+// Tile order of the v_perm kernel (k <= 3: at most 7 shard streams per stripe;
+// tools/order_sweep.sh KB_ORD "vperm ord", 7 rounds, % of 8 TB/s,
+// profiles/r01/tile_order/segments/ord_vperm): 2-stripe interleave up to 8 MiB shards
+// (RS(3,2) 1 MiB 74.9 -> 77.6, 5.6 MB 75.6 -> 80.6, RS(2,1) 64 KiB 74.9 -> 78.2, RS(2,2)
+// 4 MiB 75.9 -> 77.6; RS(1,1) 1 MiB 79.2 -> 78.4), 16 column segments above 8 MiB when
+// the shards sit at multiples of 8 MiB (RS(3,2) 16 MiB 72.7 -> 77.7), else consecutive.
+inline TileOrder vec_tile_order(uint64_t S, uint64_t tps, int addr_tz) {
+  if (tps <= 1024) return TileOrder::kGroup2;
+  if (addr_tz >= 23 && S < (128ull << 20)) return TileOrder::kSeg16;
+  return TileOrder::kConsecutive;
+}
+
+}  // namespace callfs

@@ -5,6 +5,8 @@
 //     every (c, x), i.e. what rs_apply.hpp's gf_mul4 computes
 //  3. decode_plan rows reproduce erased shards for every 1..m erasure pattern subset
 //  4. CopyPool under concurrent callers
+//  5. tile orders (tile_order.hpp): every block -> (stripe, tile) map is a bijection, and
+//     the launch rules pick the measured orders for known layouts
 #include <cstdio>
 #include <random>
 #include <cstring>
@@ -13,6 +15,7 @@
 
 #include "copy_pool.hpp"
 #include "gf256.hpp"
+#include "tile_order.hpp"
 
 using namespace callfs;
 
@@ -198,6 +201,61 @@ int main() {
       });
     for (auto& th : ts) th.join();
     CHECK(bad == 0);
+  }
+  // 5. tile orders
+  {
+    auto bijective = [](auto map, uint32_t tps, uint32_t batch) {
+      std::vector<uint8_t> seen(static_cast<size_t>(tps) * batch, 0);
+      for (uint32_t t = 0; t < tps * batch; ++t) {
+        uint32_t stripe = ~0u, tile = ~0u;
+        map(t, tps, batch, stripe, tile);
+        if (stripe >= batch || tile >= tps) return false;
+        uint8_t& c = seen[static_cast<size_t>(stripe) * tps + tile];
+        if (c++) return false;
+      }
+      return true;
+    };
+    const uint32_t tpss[] = {1, 2, 7, 8, 13, 16, 31, 32, 33, 63, 64, 100, 128, 129, 1023,
+                             1024, 1025, 1537, 2048, 2561, 4100};
+    const uint32_t batches[] = {1, 2, 3, 5, 7, 8, 9, 31, 33};
+    for (uint32_t tps : tpss)
+      for (uint32_t b : batches) {
+        CHECK(bijective(map_tile<0>, tps, b));
+        CHECK(bijective(map_tile<2>, tps, b));
+        CHECK(bijective(map_tile<3>, tps, b));
+        CHECK(bijective(map_tile<4>, tps, b));
+        CHECK(bijective(map_tile<5>, tps, b));
+        CHECK(bijective(map_tile<6>, tps, b));
+        CHECK(bijective(map_tile<7>, tps, b));
+        CHECK(bijective(map_tile<8>, tps, b));
+        CHECK(bijective(map_tile<9>, tps, b));
+      }
+    // rules, on layouts measured in DESIGN.md §5 (tps = S / 8 KiB)
+    auto tps_of = [](uint64_t S) { return (S / 16 + 511) / 512; };
+    const uint64_t MiB = 1ull << 20;
+    // bench shape RS(10,4) 1 MiB, contiguous stripes 14 MiB apart: G2
+    CHECK(lds_tile_order(MiB, tps_of(MiB), 20, 14, 14 * MiB) == TileOrder::kGroup2);
+    // 64 MiB objects, S = 6,710,887 (pitch 2^8 * odd), 14 streams: G2
+    CHECK(lds_tile_order(6710887, tps_of(6710887), 8, 14, 14 * 6711040ull) == TileOrder::kGroup2);
+    // RS(4,2) 4 MiB: consecutive (few streams); RS(16,4) 4 MiB: G2
+    CHECK(lds_tile_order(4 * MiB, tps_of(4 * MiB), 22, 6, 24 * MiB) == TileOrder::kConsecutive);
+    CHECK(lds_tile_order(4 * MiB, tps_of(4 * MiB), 22, 20, 80 * MiB) == TileOrder::kGroup2);
+    // power-of-two 16 MiB shards: Q16 with 14 streams, consecutive with 6
+    CHECK(lds_tile_order(16 * MiB, tps_of(16 * MiB), 24, 14, 224 * MiB) == TileOrder::kSeg16);
+    CHECK(lds_tile_order(16 * MiB, tps_of(16 * MiB), 24, 6, 96 * MiB) == TileOrder::kConsecutive);
+    // 64 MiB shards, 14 streams: Q8; 1 GiB column slices (pitch 2^8 * odd): consecutive
+    CHECK(lds_tile_order(64 * MiB, tps_of(64 * MiB), 26, 14, 0) == TileOrder::kSeg8);
+    CHECK(lds_tile_order(13421824, tps_of(13421824), 10, 14, 0) == TileOrder::kConsecutive);
+    // small shards: G8, unless stripes sit exactly 2 MiB (consecutive) or 1 MiB (G2) apart
+    CHECK(lds_tile_order(256 << 10, tps_of(256 << 10), 18, 14, 3584 << 10) == TileOrder::kGroup8);
+    CHECK(lds_tile_order(128 << 10, tps_of(128 << 10), 17, 16, 2 * MiB) == TileOrder::kConsecutive);
+    CHECK(lds_tile_order(128 << 10, tps_of(128 << 10), 17, 8, 1 * MiB) == TileOrder::kGroup2);
+    // wide groups: Q8 from 2 MiB; v_perm kernel: G2 up to 8 MiB, Q16 for aligned 16 MiB
+    CHECK(wide_tile_order(tps_of(4 * MiB)) == TileOrder::kSeg8);
+    CHECK(wide_tile_order(tps_of(MiB)) == TileOrder::kConsecutive);
+    CHECK(vec_tile_order(349526, tps_of(349526), 8) == TileOrder::kGroup2);
+    CHECK(vec_tile_order(16 * MiB, tps_of(16 * MiB), 24) == TileOrder::kSeg16);
+    CHECK(vec_tile_order(107374183, tps_of(107374183), 8) == TileOrder::kConsecutive);
   }
   std::printf(fails ? "FAILED %d\n" : "host_test ok\n", fails);
   return fails ? 1 : 0;

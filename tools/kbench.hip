@@ -115,7 +115,7 @@ template <int ORD>
 __global__ __launch_bounds__(512) void read_probe(ApplyArgs a) {
   const uint32_t tps = static_cast<uint32_t>((a.nvec + 511) / 512);
   uint32_t stripe, tile;
-  dev::map_tile<ORD>(blockIdx.x, tps, static_cast<uint32_t>(a.batch), stripe, tile);
+  map_tile<ORD>(blockIdx.x, tps, static_cast<uint32_t>(a.batch), stripe, tile);
   const uint64_t v = static_cast<uint64_t>(tile) * 512 + threadIdx.x;
   if (v >= a.nvec) return;
   using P = dev::Policy<4, 1, true, true, false>;
