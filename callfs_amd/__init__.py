@@ -24,6 +24,7 @@ from .erasure import (  # noqa: F401
     encode_shards,
     reconstruct,
     shard_checksum,
+    shard_layout,
     verify,
 )
 
@@ -32,5 +33,5 @@ __all__ = [
     "ErrShardCorrupted", "ErrShardNotFound", "ErrShortData", "ErrTooFewShards",
     "ErrShardNoData", "ErrShardSize", "ErrSingular", "ErrUnsupportedProfile",
     "decode_rows", "encode_matrix", "encode_shards", "reconstruct", "verify",
-    "shard_checksum",
+    "shard_checksum", "shard_layout",
 ]

@@ -118,6 +118,15 @@ def shard_checksum(data) -> str:
     return hashlib.sha256(bytes(data)).hexdigest()
 
 
+def shard_layout(data, shards) -> List[tuple]:
+    """Where and under which checksum Manager.StoreFile keeps each shard
+    (erasure/manager.go:171-184): path ".erasure/<first 8 bytes of SHA-256(object), hex>/<i>"
+    and ShardChecksum(shard). The shard files are the raw shard bytes, so files written
+    from this codec's shards are what the CPU codec reads back, and the reverse."""
+    prefix = hashlib.sha256(bytes(data)).digest()[:8].hex()
+    return [(f".erasure/{prefix}/{i}", shard_checksum(sh)) for i, sh in enumerate(shards)]
+
+
 def _addr(buf) -> int:
     """Address of a bytes-like object's first byte (read-only objects allowed)."""
     a = np.frombuffer(buf, dtype=np.uint8)

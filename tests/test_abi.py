@@ -86,3 +86,16 @@ def test_init_fails_loudly_without_gpu(native_lib):
     assert native_lib.lib.rs_init(ctypes.byref(h), 0) == native_lib.RS_E_HIP
     with pytest.raises(RuntimeError):
         native_lib.Context()
+
+
+def test_shard_layout_names_like_manager(native_lib):
+    """manager.go:171-184: shard i of an object lives at .erasure/<hex of the first 8
+    bytes of SHA-256(object)>/<i>, recorded with ShardChecksum(shard)."""
+    import hashlib
+    from callfs_amd import shard_layout
+    data = b"callfs object bytes"
+    shards = [b"a" * 5, b"b" * 5, b"\0" * 5]
+    layout = shard_layout(data, shards)
+    prefix = hashlib.sha256(data).hexdigest()[:16]
+    assert [p for p, _ in layout] == [f".erasure/{prefix}/{i}" for i in range(3)]
+    assert [c for _, c in layout] == [hashlib.sha256(s).hexdigest() for s in shards]
