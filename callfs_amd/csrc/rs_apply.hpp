@@ -168,7 +168,7 @@ void rs_apply_vec(ApplyArgs a) {
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
   const cptr<uint32_t> tabs = as_const(a.tabs);
 
-  for (uint32_t t = blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
+  for (uint32_t t = a.t_base + blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
     uint32_t stripe, tile;
     if constexpr (P::ORD == 1) {
       tile = t / static_cast<uint32_t>(a.batch);
@@ -411,7 +411,7 @@ void rs_apply_lds(ApplyArgs a) {
   // one tile per block (vec_grid), or (PERSIST) grid-stride over tiles so that the
   // table prologue is paid once per block; either way the blocks in flight cover a
   // window of consecutive t, which is what the tile order arranges
-  for (uint32_t t = blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
+  for (uint32_t t = a.t_base + blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
     uint32_t stripe, tile;
     map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
     const uint64_t v0 = static_cast<uint64_t>(tile) * BS + threadIdx.x;

@@ -64,6 +64,37 @@ int tile_order_override() {
   }();
   return v;
 }
+// Tiles per kernel launch. Blocks are dealt to the 8 XCDs round-robin and each XCD runs
+// its share in order, so over a long grid the XCDs drift apart and the tiles in flight
+// spread over more of the address space than the tile order intends. Grids of more than
+// twice about 2 GiB of shard traffic are cut into equal consecutive slices of at most
+// that much (one launch each, same tile order), which resets the drift
+// (tools/slice_tiles_sweep.sh, % of 8 TB/s, unsliced -> sliced: RS(10,4) 64 MiB objects
+// x 256 72.8 -> 75.6-75.8, 1 MiB x 1,024 75.9 -> 76.7-77.3, 1 GiB objects x 8 74.7 ->
+// 75.3-76.0, RS(4,2) 1 MiB x 2,048 75.4 -> 76.0-76.4; the bench grid, 3.5 GiB, stays
+// whole). CALLFS_RS_MAX_TILES_PER_LAUNCH sets the slice in tiles instead.
+uint32_t slice_tiles(int streams) {
+  static const long forced = [] {
+    const char* e = std::getenv("CALLFS_RS_MAX_TILES_PER_LAUNCH");
+    return e ? std::atol(e) : 0L;
+  }();
+  if (forced >= 1024) return static_cast<uint32_t>(std::min<long>(forced, 1L << 30));
+  const uint64_t tile_bytes = 8192ull * static_cast<uint64_t>(std::max(1, streams));
+  return static_cast<uint32_t>(std::max<uint64_t>(4096, (2ull << 30) / tile_bytes));
+}
+
+// Launches `grid` blocks of one kernel as consecutive slices (see slice_tiles).
+template <class Launch>
+void launch_sliced(uint32_t grid, int streams, ApplyArgs& a, Launch&& launch) {
+  const uint32_t lim = slice_tiles(streams);
+  const uint32_t nsl = grid > 2 * lim ? (grid + lim - 1) / lim : 1;
+  const uint32_t per = (grid + nsl - 1) / nsl;
+  for (uint32_t t0 = 0; t0 < grid; t0 += per) {
+    a.t_base = t0;
+    launch(std::min(per, grid - t0));
+  }
+  a.t_base = 0;
+}
 constexpr int kLdsMinRows = 5;
 constexpr int kLdsMinK = 4;
 constexpr int kPermMaxRows = 8;  // v_perm kernel instantiations (production: k <= 3, R <= 4)
@@ -155,7 +186,9 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
                           LdsWideQ8Policy::BS == LdsPolicy::BS,
                       "one grid shape for every LDS policy");
         const unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
-        hipLaunchKernelGGL(fn, dim3(gx), dim3(LdsPolicy::BS), lds, stream, a);
+        launch_sliced(gx, a.K + a.R, a, [&](uint32_t blocks) {
+          hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, a);
+        });
       } else {
         VecFn fn = kVec[a.R - 1];  // R <= 4 here (R >= kLdsMinRows takes the LDS kernel)
         const uint64_t tps = (a.nvec + ProdPolicy::BS - 1) / ProdPolicy::BS;
@@ -168,7 +201,9 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
                           ProdG2Policy::U == ProdPolicy::U && ProdQ16Policy::U == ProdPolicy::U,
                       "one grid shape for every v_perm policy");
         const unsigned gx = dev::vec_grid<ProdPolicy>(a.nvec, a.batch);
-        hipLaunchKernelGGL(fn, dim3(gx), dim3(ProdPolicy::BS), 0, stream, a);
+        launch_sliced(gx, a.K + a.R, a, [&](uint32_t blocks) {
+          hipLaunchKernelGGL(fn, dim3(blocks), dim3(ProdPolicy::BS), 0, stream, a);
+        });
       }
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;

@@ -33,6 +33,9 @@ struct ApplyArgs {
   // byte distance between consecutive stripes' shards when it is the same for every
   // stripe (0 = one stripe or irregular); also keys the tile order.
   uint64_t stripe_stride;
+  // first tile of this launch (launch_apply cuts grids of many tiles into consecutive
+  // slices; a kernel's block b works on tile t_base + b of the whole tile order)
+  uint32_t t_base;
 };
 
 // addr_tz for a set of shard addresses: trailing zeros of the OR of their differences

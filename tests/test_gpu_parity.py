@@ -443,6 +443,32 @@ def test_full_size_bench_shape_linearity_and_matrix(native_lib):
     assert torch.equal(par.amin(dim=2), want) and torch.equal(par.amax(dim=2), want)
 
 
+@pytest.mark.parametrize("k,m,batch", [(3, 2, 1024), (4, 2, 700)])
+def test_sliced_launch_grids_roundtrip(native_lib, k, m, batch):
+    """Grids of more than twice ~2 GiB of traffic run as consecutive launch slices
+    (rs_kernels.hip slice_tiles): RS(3,2) 1 MiB x 1,024 stripes (v_perm kernel, 131,072
+    tiles, 3 slices) and RS(4,2) 1 MiB x 700 (LDS kernel, 89,600 tiles, 3 slices). Every
+    stripe must round-trip; first, middle and last stripe against the oracle."""
+    import torch
+    from callfs_amd.device import Plan
+    S = 1 << 20
+    sb = _batch(k, m, S, batch, seed=batch + k)
+    Plan.for_batch(sb).launch()
+    torch.cuda.synchronize()
+    for b in (0, batch // 2, batch - 1):
+        h = sb.buf[b, :, :S].cpu().numpy()
+        want = cref.encode([h[i] for i in range(k)], k, m)
+        assert all(np.array_equal(h[k + j], want[j]) for j in range(m)), b
+    ref = sb.buf.clone()
+    erase = [0, k + m - 1]
+    for i in erase:
+        sb.buf[:, i, :S].fill_(0x33)
+    dec = Plan.for_batch(sb, present=[i not in erase for i in range(k + m)])
+    dec.launch()
+    assert not dec.corrupt()
+    assert torch.equal(sb.buf[:, :, :S], ref[:, :, :S])
+
+
 def test_full_size_config_rs10_4_64mib_roundtrip(native_lib):
     """configs[1]/[2] at full size: 256 objects of 64 MiB (S = 6,710,887; 22.4 GiB of
     shards in HBM). Encode the batch, erase 4 shards per pattern, decode, require every

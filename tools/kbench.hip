@@ -246,6 +246,19 @@ int main(int argc, char** argv) {
   vs.push_back(Variant{"prod dispatch", [](const ApplyArgs& a, hipStream_t s) {
                          CK(launch_apply(a, s));
                        }});
+  if (const char* sp = std::getenv("KB_SPLIT")) {  // same work as launches over B/N stripes each
+    static const int parts = std::max(1, std::atoi(sp));
+    vs.push_back(Variant{"prod split", [](const ApplyArgs& a, hipStream_t s) {
+                           const int per = (a.batch + parts - 1) / parts;
+                           for (int b0 = 0; b0 < a.batch; b0 += per) {
+                             ApplyArgs p = a;
+                             p.batch = std::min(per, a.batch - b0);
+                             p.in_tab = a.in_tab + static_cast<size_t>(b0) * a.K;
+                             p.out_tab = a.out_tab + static_cast<size_t>(b0) * a.R;
+                             CK(launch_apply(p, s));
+                           }
+                         }});
+  }
   if (std::getenv("KB_BYTES"))  // the byte kernel over the whole shard (unaligned-pointer dispatch)
     vs.push_back(Variant{"byte-kernel dispatch", [](const ApplyArgs& a, hipStream_t s) {
                            CK(launch_apply(a, s, /*bytes_only=*/true));

@@ -20,6 +20,12 @@ def main(src, dst, k=10, m=4, S=1 << 20, B=256, kernel="rs_apply_lds"):
         vals[name] = (statistics.median(v), len(v))
     fetch_b = vals["FETCH_SIZE"][0] * 1024 * 2
     write_b = vals["WRITE_SIZE"][0] * 1024
+    # grids of > 2 x ~2 GiB of traffic run as several dispatches per plan launch
+    # (rs_kernels.hip slice_tiles): scale per-dispatch counters to one launch
+    algo = B * S * (k + m)
+    slices = max(1, round(algo / (fetch_b + write_b)))
+    fetch_b *= slices
+    write_b *= slices
     out = {
         "config": {"k": k, "m": m, "shard_bytes": S, "stripes": B},
         "kernel": ks["Name"],
@@ -36,7 +42,8 @@ def main(src, dst, k=10, m=4, S=1 << 20, B=256, kernel="rs_apply_lds"):
         "fetch_bytes_per_launch": fetch_b,
         "write_bytes_per_launch": write_b,
         "encode_bytes_per_launch": fetch_b + write_b,
-        "algorithmic_bytes_per_launch": B * S * (k + m),
+        "algorithmic_bytes_per_launch": algo,
+        "dispatches_per_launch": slices,
     }
     trace = os.path.join(src, "kt", "kt_kernel_trace.csv")
     if os.path.exists(trace):  # per-dispatch rows of the hot kernel
