@@ -153,3 +153,22 @@ def test_golden_vectors_reproduce_with_c_oracle():
         dsh = [buf[i * S:(i + 1) * S] for i in range(k)]
         sh = dsh + cref.encode(dsh, k, m, simd=True, nthreads=4)
         assert [hashlib.sha256(s.tobytes()).hexdigest() for s in sh] == case["shard_sha256"]
+
+
+def test_configs0_rs3_2_1mib_encode_verify():
+    """BASELINE.json configs[0]: RS(3,2) encode + verify of a 1 MiB object on the CPU
+    (erasure/codec_test.go's round trip at that size): S = 349,526 with 2 bytes of Split
+    padding, Verify passes, Decode with every shard present returns the object, and the
+    per-shard SHA-256 equal the golden fixture of the same seeded input."""
+    import hashlib
+    import json
+    import os
+    vec = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "vectors.json")))
+    case = next(c for c in vec["digest"] if c["name"] == "1mib_rs3_2")
+    data = np.random.default_rng(case["seed"]).integers(0, 256, case["len"], dtype=np.uint8).tobytes()
+    shards = o.codec_encode(data, 3, 2)
+    assert [len(s) for s in shards] == [349_526] * 5
+    assert bytes(np.asarray(shards[2])[-2:]) == b"\0\0"
+    assert o.verify(shards, 3, 2)
+    assert [hashlib.sha256(np.asarray(s).tobytes()).hexdigest() for s in shards] == case["shard_sha256"]
+    assert o.codec_decode(list(shards), 3, 2, len(data)) == data
