@@ -83,10 +83,15 @@ uint32_t slice_tiles(int streams) {
   return static_cast<uint32_t>(std::max<uint64_t>(4096, (2ull << 30) / tile_bytes));
 }
 
-// Launches `grid` blocks of one kernel as consecutive slices (see slice_tiles).
+// Launches `grid` blocks of one kernel as consecutive slices (see slice_tiles). Launches
+// that only compare (every row a Verify row, no stores) stay whole: read-only streams
+// lose ≈ 1 point to the slice drains and gain nothing (configs[2] shape with nothing
+// erased: 79.0-79.4 % whole vs 78.0-78.4 % sliced).
 template <class Launch>
 void launch_sliced(uint32_t grid, int streams, ApplyArgs& a, Launch&& launch) {
-  const uint32_t lim = slice_tiles(streams);
+  const uint32_t all_rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
+  const bool read_only = (a.verify_mask & all_rows) == all_rows;
+  const uint32_t lim = read_only ? grid : slice_tiles(streams);
   const uint32_t nsl = grid > 2 * lim ? (grid + lim - 1) / lim : 1;
   const uint32_t per = (grid + nsl - 1) / nsl;
   for (uint32_t t0 = 0; t0 < grid; t0 += per) {
