@@ -43,6 +43,21 @@ namespace {
     if ((x) != hipSuccess) return RS_E_HIP; \
   } while (0)
 
+// Restores the calling thread's current HIP device on scope exit: entry points select
+// the device they work on, and a caller's later default-device work (torch, HIP) must
+// not land on another GPU because of a codec call.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 constexpr size_t kPitchAlign = 256;
 constexpr int kMaxLanesPerDevice = 8;
 
@@ -759,10 +774,13 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
       HIPCHK(hipMemcpyAsync(d + cpitch * in_lo, h + cpitch * in_lo, bytes,
                             hipMemcpyHostToDevice, sl.stream));
     } else {
-      for (const auto& r : in_runs)
-        HIPCHK(hipMemcpyAsync(d + cpitch * r.first, h + cpitch * r.first,
-                              cpitch * (r.second - r.first) + w, hipMemcpyHostToDevice,
-                              sl.stream));
+      // one copy per run of consecutive shard indices of every stripe in the chunk
+      for (int b = 0; b < cnt; ++b)
+        for (const auto& r : in_runs) {
+          const size_t o = spitch * b + cpitch * r.first;
+          HIPCHK(hipMemcpyAsync(d + o, h + o, cpitch * (r.second - r.first) + w,
+                                hipMemcpyHostToDevice, sl.stream));
+        }
     }
     if (verify) HIPCHK(hipMemsetAsync(dstatus, 0, sizeof(int) * cnt, sl.stream));
     HIPCHK(launch_groups(t, ML, cnt, meta, w, sl.stream, 1, sl.meta_hint));
@@ -772,10 +790,12 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
         HIPCHK(hipMemcpyAsync(h + cpitch * out_lo, d + cpitch * out_lo, bytes,
                               hipMemcpyDeviceToHost, sl.stream));
       } else {
-        for (const auto& r : out_runs)
-          HIPCHK(hipMemcpyAsync(h + cpitch * r.first, d + cpitch * r.first,
-                                cpitch * (r.second - r.first) + w, hipMemcpyDeviceToHost,
-                                sl.stream));
+        for (int b = 0; b < cnt; ++b)
+          for (const auto& r : out_runs) {
+            const size_t o = spitch * b + cpitch * r.first;
+            HIPCHK(hipMemcpyAsync(h + o, d + o, cpitch * (r.second - r.first) + w,
+                                  hipMemcpyDeviceToHost, sl.stream));
+          }
       }
     }
     if (verify)
@@ -890,7 +910,10 @@ int rs_init(rs_ctx** out, unsigned device_mask) {
   return RS_OK;
 }
 
-void rs_shutdown(rs_ctx* ctx) { delete ctx; }
+void rs_shutdown(rs_ctx* ctx) {
+  DeviceGuard dg;
+  delete ctx;
+}
 
 int rs_device_count(const rs_ctx* ctx) { return ctx ? static_cast<int>(ctx->devs.size()) : 0; }
 
@@ -951,6 +974,7 @@ int rs_decode_rows(int k, int m, const uint8_t* present, int* valid_out, int* mi
 
 int rs_encode(rs_ctx* ctx, int k, int m, size_t S, const uint8_t* const* data,
               uint8_t* const* parity) {
+  DeviceGuard dg;
   int rc = check_profile(k, m);
   if (rc) return rc;
   if (!ctx || !data || !parity) return RS_E_ARG;
@@ -965,11 +989,15 @@ int rs_encode(rs_ctx* ctx, int k, int m, size_t S, const uint8_t* const* data,
 
 int rs_codec_encode(rs_ctx* ctx, int k, int m, const uint8_t* data, size_t len,
                     uint8_t* shards_out, size_t out_cap, size_t* shard_size) {
-  // codec.go:22-24 profile check, :26 New, :31 Split, :36 Encode
-  int rc = check_profile(k, m);
-  if (rc) return rc;
+  DeviceGuard dg;
+  // codec.go:22-24 profile check, :26 New, :31 Split, :36 Encode. Upstream New accepts
+  // k+m > 256 (Leopard), so an empty object fails in Split before the profile is
+  // found unsupported here.
+  if (k < 1 || m < 1) return RS_E_INVALID_PROFILE;
   if (!ctx || !shard_size || (len && (!data || !shards_out))) return RS_E_ARG;
   if (len == 0) return RS_E_SHORT_DATA;
+  int rc = check_profile(k, m);
+  if (rc) return rc;
   const size_t S = (len + k - 1) / k;
   const int n = k + m;
   if (out_cap < S * n) return RS_E_ARG;
@@ -1000,6 +1028,7 @@ int rs_codec_encode(rs_ctx* ctx, int k, int m, const uint8_t* data, size_t len,
 }
 
 int rs_reconstruct(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens) {
+  DeviceGuard dg;
   int rc = check_profile(k, m);
   if (rc) return rc;
   if (!ctx || !shards || !lens) return RS_E_ARG;
@@ -1008,6 +1037,7 @@ int rs_reconstruct(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* le
 
 int rs_verify(rs_ctx* ctx, int k, int m, const uint8_t* const* shards, const size_t* lens,
               int* ok) {
+  DeviceGuard dg;
   int rc = check_profile(k, m);
   if (rc) return rc;
   if (!ctx || !shards || !lens || !ok) return RS_E_ARG;
@@ -1030,6 +1060,7 @@ int rs_verify(rs_ctx* ctx, int k, int m, const uint8_t* const* shards, const siz
 
 int rs_codec_decode(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* lens,
                     uint8_t* out, int64_t original_size) {
+  DeviceGuard dg;
   // codec.go:46-48 profile, :50 New, :55 Reconstruct, :59-65 Verify, :67-77 join/trim
   int rc = check_profile(k, m);
   if (rc) return rc;
@@ -1081,6 +1112,7 @@ int first_error(const int* status, int batch) {
 
 int rs_encode_batch(rs_ctx* ctx, int k, int m, int batch, const size_t* sizes,
                     const uint8_t* const* data, uint8_t* const* parity, int* status) {
+  DeviceGuard dg;
   int rc = check_profile(k, m);
   if (rc) return rc;
   if (!ctx || batch < 0 || (batch && (!sizes || !data || !parity || !status))) return RS_E_ARG;
@@ -1107,6 +1139,7 @@ int rs_encode_batch(rs_ctx* ctx, int k, int m, int batch, const size_t* sizes,
 
 int rs_reconstruct_batch(rs_ctx* ctx, int k, int m, int batch, uint8_t* const* shards,
                          size_t* lens, int verify, int* status) {
+  DeviceGuard dg;
   int rc = check_profile(k, m);
   if (rc) return rc;
   if (!ctx || batch < 0 || (batch && (!shards || !lens || !status))) return RS_E_ARG;
@@ -1174,6 +1207,7 @@ struct rs_plan {
 
 int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
                    const uint8_t* present, uint8_t* const* shards, rs_plan** out) {
+  DeviceGuard dg;
   int rc = check_profile(k, m);
   if (rc) return rc;
   if (!ctx || !shards || !out || batch < 1) return RS_E_ARG;
@@ -1212,6 +1246,7 @@ int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
 }
 
 int rs_plan_launch(rs_plan* plan, void* stream) {
+  DeviceGuard dg;
   if (!plan) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
   HIPCHK(launch_groups(*plan->tables, plan->layout, plan->batch,
@@ -1221,6 +1256,7 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
 }
 
 int rs_plan_stripe_status(rs_plan* plan, void* stream, int* flags) {
+  DeviceGuard dg;
   if (!plan || !flags) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
   auto s = static_cast<hipStream_t>(stream);
@@ -1244,6 +1280,7 @@ int rs_plan_status(rs_plan* plan, void* stream, int* corrupt) {
 uint64_t rs_plan_bytes(const rs_plan* plan) { return plan ? plan->bytes : 0; }
 
 void rs_plan_destroy(rs_plan* plan) {
+  DeviceGuard dg;
   if (!plan) return;
   (void)hipSetDevice(plan->device);
   if (plan->dmeta) (void)hipFree(plan->dmeta);
@@ -1285,6 +1322,7 @@ struct rs_hash_plan {
 
 int rs_sha256_plan_create(rs_ctx* ctx, int device, const uint8_t* const* msgs,
                           const uint64_t* lens, int count, rs_hash_plan** out) {
+  DeviceGuard dg;
   if (!ctx || !out || count < 0 || (count && (!msgs || !lens))) return RS_E_ARG;
   *out = nullptr;
   if (!ctx->device(device)) return RS_E_ARG;
@@ -1310,6 +1348,7 @@ int rs_sha256_plan_create(rs_ctx* ctx, int device, const uint8_t* const* msgs,
 }
 
 int rs_sha256_plan_launch(rs_hash_plan* plan, uint8_t* digests, void* stream) {
+  DeviceGuard dg;
   if (!plan || (plan->count && !digests)) return RS_E_ARG;
   if ((reinterpret_cast<uintptr_t>(digests) & 3u) != 0) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
@@ -1324,6 +1363,7 @@ int rs_sha256_plan_launch(rs_hash_plan* plan, uint8_t* digests, void* stream) {
 }
 
 void rs_sha256_plan_destroy(rs_hash_plan* plan) {
+  DeviceGuard dg;
   if (!plan) return;
   (void)hipSetDevice(plan->device);
   if (plan->dtab) (void)hipFree(plan->dtab);

@@ -159,12 +159,14 @@ class Codec:
         k, m = profile.data_shards, profile.parity_shards
         if k < 1 or m < 1:
             raise ErrInvalidProfile()
-        if k + m > 256:
-            raise _wrapped(N.RS_E_UNSUPPORTED, "erasure: failed to create encoder")
         src = memoryview(data).cast("B")
         L = len(src)
+        # upstream New succeeds for k+m > 256 (Leopard GF(2^16)), so an empty object
+        # still fails in Split first (codec.go:26 then :31)
         if L == 0:
             raise ErrShortData(f"erasure: failed to split data: {ErrShortData.text}")
+        if k + m > 256:
+            raise _wrapped(N.RS_E_UNSUPPORTED, "erasure: failed to create encoder")
         S = (L + k - 1) // k
         full = L // S  # data shards lying entirely inside `data`
         tail = bytearray(S * (k - full))
@@ -314,17 +316,21 @@ def reconstruct_batch(stripes: List[List], k: int, m: int, verify: bool = True,
     ctx = context or N.default_context()
     n = k + m
     B = len(stripes)
-    flat, lens = [], (ctypes.c_size_t * max(B * n, 1))()
+    if any(len(st) != n for st in stripes):
+        raise ErrTooFewShards()
+    # missing entries get fresh buffers in a per-stripe copy (upstream Reconstruct
+    # allocates them); the caller's lists change only for stripes that succeeded
+    flat, lens, bufs = [], (ctypes.c_size_t * max(B * n, 1))(), []
     for b, st in enumerate(stripes):
-        if len(st) != n:
-            raise ErrTooFewShards()
         ln = [0 if s is None else len(s) for s in st]
         S = next((x for x in ln if x), 0)
+        cp = list(st)
         for i in range(n):
             lens[b * n + i] = ln[i]
             if ln[i] == 0 and S:
-                st[i] = bytearray(S)  # upstream Reconstruct allocates missing shards
-        flat += st
+                cp[i] = bytearray(S)
+        bufs.append(cp)
+        flat += cp
     status = (ctypes.c_int * max(B, 1))()
     rc = N.lib.rs_reconstruct_batch(ctx.handle, k, m, B, _shard_ptrs(flat or [None]), lens,
                                     int(verify), status)
@@ -333,11 +339,11 @@ def reconstruct_batch(stripes: List[List], k: int, m: int, verify: bool = True,
         if not (rc == N.RS_E_ARG and any(s == N.RS_E_ARG for s in list(status)[:B])):
             N.check(rc, "rs_reconstruct_batch")
     out = list(status)[:B]
-    for b, st in enumerate(stripes):  # stripes that failed keep their missing entries
-        if out[b] not in (N.RS_OK, N.RS_E_CORRUPT):
+    for b, st in enumerate(stripes):
+        if out[b] in (N.RS_OK, N.RS_E_CORRUPT):
             for i in range(n):
-                if lens[b * n + i] == 0:
-                    st[i] = None
+                if st[i] is None or len(st[i]) == 0:
+                    st[i] = bufs[b][i]
     return out
 
 

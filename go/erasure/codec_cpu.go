@@ -1,0 +1,18 @@
+//go:build !(rocm && cgo)
+
+package erasure
+
+// Builds without the GPU codec (the default CGO_ENABLED=0 release builds,
+// Dockerfile:20-22, builds.sh:8-20) keep the reference codec: after codec.go.diff its
+// methods are named cpuEncode / cpuDecode, and these two forward to them, so the binary
+// behaves exactly as before.
+
+// Encode splits data into DataShards pieces and computes ParityShards parity shards.
+func (c *Codec) Encode(data []byte, profile ErasureProfile) ([][]byte, error) {
+	return c.cpuEncode(data, profile)
+}
+
+// Decode reconstructs the original data from shards (nil entries are missing).
+func (c *Codec) Decode(shards [][]byte, profile ErasureProfile, originalSize int64) ([]byte, error) {
+	return c.cpuDecode(shards, profile, originalSize)
+}

@@ -39,6 +39,11 @@ def lib():
                                       P(ctypes.c_void_p), u8p]
         L.orc_verify.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, P(ctypes.c_void_p)]
         L.orc_simd_kind.restype = ctypes.c_int
+        L.orc_bench_codec.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, u8p,
+                                      ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, u8p,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                      P(ctypes.c_double), P(ctypes.c_int)]
+        L.orc_bench_codec.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -92,6 +97,30 @@ def verify(shards, k: int, m: int) -> bool:
     S = len(shards[0])
     arr = [np.ascontiguousarray(s, dtype=np.uint8) for s in shards]
     return bool(lib().orc_verify(k, m, S, _ptrs(arr)))
+
+
+BENCH_ENCODE, BENCH_RECONSTRUCT, BENCH_VERIFY = 1, 2, 4
+BENCH_MODES = {"stripe-parallel": 0, "byte-range": 1}
+
+
+def bench_codec(buf: np.ndarray, k: int, m: int, S: int, present=None,
+                ops: int = BENCH_ENCODE | BENCH_RECONSTRUCT | BENCH_VERIFY,
+                mode: str = "stripe-parallel", nthreads: int = 1, seconds: float = 1.0):
+    """Native timing loop of the reference's per-object work (rs_oracle.c
+    orc_bench_codec) over buf = uint8 [stripes][k+m][pitch] (C-contiguous; shards are
+    the first S bytes of each row). Erased shards (present[i] false) are reconstructed
+    in place. Returns (verify_mismatches, elapsed_seconds, passes)."""
+    assert buf.dtype == np.uint8 and buf.ndim == 3 and buf.flags.c_contiguous
+    ns, n, pitch = buf.shape
+    assert n == k + m and S <= pitch
+    pr = None if present is None else np.array([1 if p else 0 for p in present], np.uint8)
+    el, passes = ctypes.c_double(0), ctypes.c_int(0)
+    rc = lib().orc_bench_codec(k, m, S, _u8(buf), n * pitch, pitch, ns,
+                               None if pr is None else _u8(pr), ops, BENCH_MODES[mode],
+                               nthreads, seconds, ctypes.byref(el), ctypes.byref(passes))
+    if rc < 0:
+        raise ValueError(f"orc_bench_codec rc={rc}")
+    return rc, el.value, passes.value
 
 
 def simd_kind() -> str:

@@ -27,6 +27,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <immintrin.h>
 
 static uint8_t g_exp[512];
@@ -422,4 +423,252 @@ void orc_apply_simd(int rows, int k, const uint8_t* coef, size_t S,
     else pool_run(jobs, njobs);
     free(jobs); free(mats); free(lo); free(hi);
   }
+}
+
+/* ------------------------------------------------------------------------------------
+ * CPU baseline driver: the reference's per-object work timed natively (no per-shard
+ * Python calls). For each stripe of a [stripe][n][S] buffer:
+ *   ops & 1  Encode       parity = P . data                        (codec.go:36)
+ *   ops & 2  Reconstruct  erased data from the first k present,
+ *                         then erased parity from data             (codec.go:55)
+ *   ops & 4  Verify       P . data into a temporary, compared with
+ *                         the stored parity (bytes.Equal)          (codec.go:59)
+ * Erased shards are rewritten in place (upstream reuses a nil entry's capacity).
+ * mode 0 "stripe-parallel": each thread takes whole stripes (independent requests on
+ *        separate goroutines, manager.go:60 shares one Codec);
+ * mode 1 "byte-range": every op of every stripe is split over all threads by 64-B
+ *        aligned byte ranges with a join after each op (upstream codeSomeShardsP).
+ * Returns the number of Verify mismatches (stripes x parity rows), or < 0 on error.
+ * ------------------------------------------------------------------------------------ */
+
+typedef struct {
+  int rows, k;
+  uint8_t coef[MAX_ROWS_SIMD * 256];
+  uint64_t mats[MAX_ROWS_SIMD * 256];
+  uint8_t lo[MAX_ROWS_SIMD * 256 * 16], hi[MAX_ROWS_SIMD * 256 * 16];
+} rowset_t;
+
+static void rowset_prep(rowset_t* rs, int rows, int k, const uint8_t* coef) {
+  rs->rows = rows;
+  rs->k = k;
+  for (int t = 0; t < rows * k; t++) {
+    rs->coef[t] = coef[t];
+    rs->mats[t] = gfni_matrix(coef[t]);
+    for (int x = 0; x < 16; x++) {
+      rs->lo[t * 16 + x] = g_mul[coef[t]][x];
+      rs->hi[t * 16 + x] = g_mul[coef[t]][x << 4];
+    }
+  }
+}
+
+static void rowset_apply(const rowset_t* rs, int kind, size_t b0, size_t b1,
+                         const uint8_t* const* in, uint8_t* const* out) {
+  job_t j;
+  j.rows = rs->rows; j.k = rs->k; j.kind = kind;
+  j.coef = rs->coef; j.mats = rs->mats; j.lo = rs->lo; j.hi = rs->hi;
+  j.b0 = b0; j.b1 = b1; j.in = in; j.out = out;
+  run_range(&j);
+}
+
+#define BENCH_MAX_SETS 64 /* ceil(256 / MAX_ROWS_SIMD) row sets per matrix */
+
+typedef struct {
+  int k, m, n, kind, ops, mode, nthreads;
+  size_t S, stripe_pitch, shard_pitch;
+  uint8_t* buf;
+  int nstripes;
+  int valid[256], nmiss_d, miss_d[256], nmiss_p, miss_p[256];
+  rowset_t* enc;  int nenc;   /* P, MAX_ROWS_SIMD rows per set */
+  rowset_t* dec;  int ndec;   /* inv(E[valid]) rows of the erased data shards */
+  rowset_t* par;  int npar;   /* P rows of the erased parity shards */
+  uint8_t** tmp;              /* per-thread m x S verify temporaries (mode 0) or one */
+  /* phase state */
+  pthread_barrier_t start, end;
+  volatile int stop;
+  int cur_stripe, cur_op, njobs;
+  size_t per;
+  int next; /* atomic */
+  int mismatches; /* atomic */
+} bench_t;
+
+static void bench_op(bench_t* B, int s, int op, size_t b0, size_t b1, uint8_t* tmp) {
+  uint8_t* base = B->buf + (size_t)s * B->stripe_pitch;
+  const uint8_t* in[256];
+  uint8_t* out[256];
+  for (int i = 0; i < B->n; i++) in[i] = base + (size_t)i * B->shard_pitch;
+  if (op == 1) {
+    for (int g = 0; g < B->nenc; g++) {
+      for (int r = 0; r < B->enc[g].rows; r++)
+        out[r] = base + (size_t)(B->k + g * MAX_ROWS_SIMD + r) * B->shard_pitch;
+      rowset_apply(&B->enc[g], B->kind, b0, b1, in, out);
+    }
+  } else if (op == 2) {
+    const uint8_t* vin[256];
+    for (int i = 0; i < B->k; i++) vin[i] = in[B->valid[i]];
+    for (int g = 0; g < B->ndec; g++) {
+      for (int r = 0; r < B->dec[g].rows; r++)
+        out[r] = base + (size_t)B->miss_d[g * MAX_ROWS_SIMD + r] * B->shard_pitch;
+      rowset_apply(&B->dec[g], B->kind, b0, b1, vin, out);
+    }
+    for (int g = 0; g < B->npar; g++) {
+      for (int r = 0; r < B->par[g].rows; r++)
+        out[r] = base + (size_t)B->miss_p[g * MAX_ROWS_SIMD + r] * B->shard_pitch;
+      rowset_apply(&B->par[g], B->kind, b0, b1, in, out);
+    }
+  } else if (op == 4) {
+    for (int g = 0; g < B->nenc; g++) {
+      for (int r = 0; r < B->enc[g].rows; r++)
+        out[r] = tmp + (size_t)(g * MAX_ROWS_SIMD + r) * B->S;
+      rowset_apply(&B->enc[g], B->kind, b0, b1, in, out);
+    }
+    int bad = 0;
+    for (int j = 0; j < B->m; j++)
+      bad += memcmp(tmp + (size_t)j * B->S + b0, in[B->k + j] + b0, b1 - b0) != 0;
+    if (bad) __atomic_fetch_add(&B->mismatches, bad, __ATOMIC_RELAXED);
+  }
+}
+
+static void bench_work(bench_t* B, int tid) {
+  for (;;) {
+    int j = __atomic_fetch_add(&B->next, 1, __ATOMIC_RELAXED);
+    if (j >= B->njobs) return;
+    if (B->mode == 0) {
+      for (int op = 1; op <= 4; op <<= 1)
+        if (B->ops & op) bench_op(B, j, op, 0, B->S, B->tmp[tid]);
+    } else {
+      size_t b0 = (size_t)j * B->per, b1 = b0 + B->per < B->S ? b0 + B->per : B->S;
+      bench_op(B, B->cur_stripe, B->cur_op, b0, b1, B->tmp[0]);
+    }
+  }
+}
+
+typedef struct { bench_t* B; int tid; } bench_arg_t;
+
+static void* bench_thread(void* p) {
+  bench_arg_t* a = (bench_arg_t*)p;
+  for (;;) {
+    pthread_barrier_wait(&a->B->start);
+    if (a->B->stop) return NULL;
+    bench_work(a->B, a->tid);
+    pthread_barrier_wait(&a->B->end);
+  }
+}
+
+/* One phase on all threads: `njobs` jobs (stripes in mode 0, byte ranges in mode 1). */
+static void bench_phase(bench_t* B, int njobs) {
+  B->njobs = njobs;
+  __atomic_store_n(&B->next, 0, __ATOMIC_RELAXED);
+  pthread_barrier_wait(&B->start);
+  bench_work(B, 0);
+  pthread_barrier_wait(&B->end);
+}
+
+static void bench_pass(bench_t* B) {
+  if (B->mode == 0) {
+    bench_phase(B, B->nstripes);
+    return;
+  }
+  const int nr = (int)((B->S + B->per - 1) / B->per);
+  for (int s = 0; s < B->nstripes; s++)
+    for (int op = 1; op <= 4; op <<= 1)
+      if (B->ops & op) {
+        B->cur_stripe = s;
+        B->cur_op = op;
+        bench_phase(B, nr);
+      }
+}
+
+static double mono_now(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + (double)t.tv_nsec * 1e-9;
+}
+
+static rowset_t* make_sets(int rows, int k, const uint8_t* coef, int* nsets) {
+  *nsets = (rows + MAX_ROWS_SIMD - 1) / MAX_ROWS_SIMD;
+  if (*nsets == 0) return NULL;
+  rowset_t* s = (rowset_t*)calloc((size_t)*nsets, sizeof(rowset_t));
+  for (int g = 0; g < *nsets; g++) {
+    int rr = rows - g * MAX_ROWS_SIMD < MAX_ROWS_SIMD ? rows - g * MAX_ROWS_SIMD : MAX_ROWS_SIMD;
+    rowset_prep(&s[g], rr, k, coef + (size_t)g * MAX_ROWS_SIMD * k);
+  }
+  return s;
+}
+
+int orc_bench_codec(int k, int m, size_t S, uint8_t* buf, size_t stripe_pitch,
+                    size_t shard_pitch, int nstripes, const uint8_t* present, int ops,
+                    int mode, int nthreads, double seconds, double* elapsed_out,
+                    int* passes_out) {
+  ensure_init();
+  if (k < 1 || m < 1 || k + m > 256 || !buf || nstripes < 1 || S == 0 || nthreads < 1 ||
+      nthreads > POOL_MAX || (mode != 0 && mode != 1))
+    return -1;
+  bench_t* B = (bench_t*)calloc(1, sizeof(bench_t));
+  B->k = k; B->m = m; B->n = k + m; B->S = S; B->buf = buf;
+  B->stripe_pitch = stripe_pitch; B->shard_pitch = shard_pitch; B->nstripes = nstripes;
+  B->ops = ops; B->mode = mode; B->nthreads = nthreads; B->kind = orc_simd_kind();
+  uint8_t* E = (uint8_t*)malloc((size_t)B->n * k);
+  uint8_t* sub = (uint8_t*)malloc((size_t)k * k);
+  uint8_t* inv = (uint8_t*)malloc((size_t)k * k);
+  uint8_t* drows = (uint8_t*)malloc((size_t)k * k);
+  uint8_t* prows = (uint8_t*)malloc((size_t)m * k);
+  int rc = -1;
+  if (orc_encode_matrix(k, m, E)) goto out;
+  int np = 0;
+  for (int i = 0; i < B->n; i++)
+    if (!present || present[i]) { if (np < k) B->valid[np] = i; np++; }
+  if (np < k) { rc = -2; goto out; }
+  for (int r = 0; r < k; r++) memcpy(sub + (size_t)r * k, E + (size_t)B->valid[r] * k, k);
+  if (orc_invert(k, sub, inv)) { rc = -3; goto out; }
+  for (int i = 0; i < B->n; i++) {
+    if (present && present[i]) continue;
+    if (!present) break;
+    if (i < k) {
+      memcpy(drows + (size_t)B->nmiss_d * k, inv + (size_t)i * k, k);
+      B->miss_d[B->nmiss_d++] = i;
+    } else {
+      memcpy(prows + (size_t)B->nmiss_p * k, E + (size_t)i * k, k);
+      B->miss_p[B->nmiss_p++] = i;
+    }
+  }
+  B->enc = make_sets(m, k, E + (size_t)k * k, &B->nenc);
+  B->dec = make_sets(B->nmiss_d, k, drows, &B->ndec);
+  B->par = make_sets(B->nmiss_p, k, prows, &B->npar);
+  B->tmp = (uint8_t**)calloc((size_t)nthreads, sizeof(uint8_t*));
+  for (int t = 0; t < (mode == 0 ? nthreads : 1); t++) B->tmp[t] = (uint8_t*)malloc((size_t)m * S);
+  /* byte ranges: 64-B aligned, at least 4 KiB, one per thread */
+  B->per = (S + nthreads - 1) / nthreads;
+  B->per = (B->per + 63) & ~(size_t)63;
+  if (B->per < 4096) B->per = 4096;
+  pthread_barrier_init(&B->start, NULL, (unsigned)nthreads);
+  pthread_barrier_init(&B->end, NULL, (unsigned)nthreads);
+  pthread_t th[POOL_MAX];
+  bench_arg_t args[POOL_MAX];
+  for (int t = 1; t < nthreads; t++) {
+    args[t].B = B;
+    args[t].tid = t;
+    pthread_create(&th[t], NULL, bench_thread, &args[t]);
+  }
+  int passes = 0;
+  const double t0 = mono_now();
+  double el;
+  do {
+    bench_pass(B);
+    passes++;
+  } while ((el = mono_now() - t0) < seconds);
+  B->stop = 1;
+  pthread_barrier_wait(&B->start);
+  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+  pthread_barrier_destroy(&B->start);
+  pthread_barrier_destroy(&B->end);
+  if (elapsed_out) *elapsed_out = el;
+  if (passes_out) *passes_out = passes;
+  rc = B->mismatches;
+  for (int t = 0; t < nthreads; t++) free(B->tmp[t]);
+  free(B->tmp);
+  free(B->enc); free(B->dec); free(B->par);
+out:
+  free(E); free(sub); free(inv); free(drows); free(prows);
+  free(B);
+  return rc;
 }

@@ -324,6 +324,16 @@ def decode_rows(k: int, m: int, present):
 # Known-answer values (upstream reedsolomon tests)
 # --------------------------------------------------------------------------------------
 
+# Provenance (none of these files is in /root/reference; the values are upstream's
+# published test constants for klauspost/reedsolomon v1.13.3, recalled, as SURVEY.md
+# 8(c) records -- nothing reference-held pins parity bytes):
+#   gal_mul, gal_exp, gal_mul_slice  galois_test.go TestGalois (galMultiply, galExp,
+#                                    galMulSlice with c = 25)
+#   one_encode                       reedsolomon_test.go TestOneEncode, RS(5,5)
+#   parity_rows                      rows of buildMatrix's E[k:] for these profiles
+# tests/test_oracle.py also checks the field and the matrix construction without any
+# recalled value: every product against a carry-less multiply reduced mod 0x11D, and
+# every row of E = V . inv(V[0:k]) for every k against the Lagrange closed form.
 KATS = {
     "gal_mul": [((3, 4), 12), ((7, 7), 21), ((23, 45), 41)],
     "gal_exp": [((2, 2), 4), ((5, 20), 235), ((13, 7), 43)],

@@ -99,3 +99,29 @@ def test_shard_layout_names_like_manager(native_lib):
     prefix = hashlib.sha256(data).hexdigest()[:16]
     assert [p for p, _ in layout] == [f".erasure/{prefix}/{i}" for i in range(3)]
     assert [c for _, c in layout] == [hashlib.sha256(s).hexdigest() for s in shards]
+
+
+def test_encode_error_precedence_matches_upstream(native_lib):
+    """codec.go:22-33: profile check, then New (accepts k+m > 256: Leopard), then Split.
+    An empty object fails with ErrShortData even for a k+m > 256 profile; a non-empty
+    one reports the unsupported (Leopard) profile. No device work happens on these
+    paths, so this runs without a GPU."""
+    from callfs_amd import Codec, ErasureProfile
+    from callfs_amd.erasure import ErrInvalidProfile, ErrShortData, ErrUnsupportedProfile
+    c = Codec()
+    with pytest.raises(ErrInvalidProfile):
+        c.encode(b"", ErasureProfile(0, 4))
+    with pytest.raises(ErrShortData):
+        c.encode(b"", ErasureProfile(200, 100))
+    with pytest.raises(ErrUnsupportedProfile):
+        c.encode(b"x", ErasureProfile(200, 100))
+    ss = ctypes.c_size_t(0)
+    buf = (ctypes.c_uint8 * 16)()
+    fake_ctx = ctypes.c_void_p(1)  # never dereferenced on these error paths
+    lib = native_lib.lib
+    assert lib.rs_codec_encode(fake_ctx, 0, 4, buf, 0, buf, 16, ctypes.byref(ss)) == \
+        native_lib.RS_E_INVALID_PROFILE
+    assert lib.rs_codec_encode(fake_ctx, 200, 100, None, 0, None, 0, ctypes.byref(ss)) == \
+        native_lib.RS_E_SHORT_DATA
+    assert lib.rs_codec_encode(fake_ctx, 200, 100, buf, 1, buf, 16, ctypes.byref(ss)) == \
+        native_lib.RS_E_UNSUPPORTED

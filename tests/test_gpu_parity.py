@@ -636,10 +636,31 @@ def test_encode_batch_chunk_shapes(native_lib, k, m, S, B):
     stripes = [[rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] for _ in range(B)]
     parity, status = E.encode_batch(stripes, k, m)
     assert status == [0] * B
-    for b in sorted({0, B // 2, B - 1}):
+    for b in range(B):  # every stripe: the 2nd+ stripe of a chunk has its own offsets
         want = cref.encode(stripes[b], k, m)
         for j in range(m):
             assert bytes(parity[b][j]) == bytes(want[j]), (b, j)
+
+
+@pytest.mark.parametrize("k,m,S,B,erase", [(4, 2, 1 << 20, 5, (0, 5)),      # 2 stripes / chunk
+                                           (4, 2, 1 << 20, 5, (1,)),        # + verify rows
+                                           (10, 4, 400_000, 7, (2, 3, 11))])
+def test_reconstruct_batch_chunk_shapes(native_lib, k, m, S, B, erase):
+    """Staged reconstruct with several stripes per chunk and per-run DMA (spitch > 4 MiB):
+    every stripe's reconstructed shards and verify flag, not only the first of a chunk."""
+    from callfs_amd import erasure as E
+    rng = np.random.default_rng(S + B + len(erase))
+    full = []
+    for _ in range(B):
+        data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+        full.append(data + cref.encode(data, k, m))
+    stripes = [[None if i in erase else bytearray(x.tobytes()) for i, x in enumerate(f)]
+               for f in full]
+    status = E.reconstruct_batch(stripes, k, m, verify=True)
+    assert status == [0] * B
+    for b in range(B):
+        for i in range(k + m):
+            assert bytes(stripes[b][i]) == full[b][i].tobytes(), (b, i)
 
 
 def test_reconstruct_batch_mixed_patterns_and_errors(native_lib):

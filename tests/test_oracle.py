@@ -172,3 +172,80 @@ def test_configs0_rs3_2_1mib_encode_verify():
     assert o.verify(shards, 3, 2)
     assert [hashlib.sha256(np.asarray(s).tobytes()).hexdigest() for s in shards] == case["shard_sha256"]
     assert o.codec_decode(list(shards), 3, 2, len(data)) == data
+
+
+# ---- checks that need no recalled value --------------------------
+
+def _clmul_mod_11d(a, b):
+    """Carry-less product of byte arrays reduced mod x^8+x^4+x^3+x^2+1 (0x11D): the
+    field's definition, with no log/exp tables."""
+    a = a.astype(np.int64)
+    b = b.astype(np.int64)
+    acc = np.zeros(np.broadcast(a, b).shape, np.int64)
+    for i in range(8):
+        acc ^= np.where((b >> i) & 1, a << i, 0)
+    for bit in range(14, 7, -1):
+        acc ^= np.where((acc >> bit) & 1, 0x11D << (bit - 8), 0)
+    return acc
+
+
+def _independent_log_exp():
+    """log/exp of the generator 2 built by repeated clmul (not the oracle's tables)."""
+    exp = np.zeros(255, np.int64)
+    log = np.full(256, -1, np.int64)
+    x = 1
+    for i in range(255):
+        exp[i] = x
+        log[x] = i
+        x = int(_clmul_mod_11d(np.array(x), np.array(2)))
+    assert sorted(exp.tolist()) == list(range(1, 256))  # 2 generates GF(2^8)*
+    return exp, log
+
+
+def test_gal_mul_exhaustive_vs_clmul():
+    a, b = np.meshgrid(np.arange(256), np.arange(256), indexing="ij")
+    want = _clmul_mod_11d(a, b)
+    got_np = np.array([[o.gal_mul(x, y) for y in range(256)] for x in range(256)])
+    assert (got_np == want).all()
+    L = cref.lib()
+    got_c = np.array([[L.orc_gal_mul(x, y) for y in range(256)] for x in range(256)])
+    assert (got_c == want).all()
+
+
+def _lagrange_matrix(k, exp, log):
+    """E[r][i] = prod_{j<k, j!=i} (r ^ j) / (i ^ j) for r in 0..255 (r < k: identity
+    rows): the unique matrix mapping values at the points 0..k-1 of a polynomial of
+    degree < k to its value at r, which is what E = V . inv(V[0:k]) is, V[r][c] = r^c."""
+    E = np.zeros((256, k), np.int64)
+    E[np.arange(k), np.arange(k)] = 1
+    if k == 256:
+        return E
+    i = np.arange(k)
+    r = np.arange(k, 256)
+    lr = log[r[:, None] ^ i[None, :]]            # (256-k, k): log(r ^ j), all nonzero
+    tot = lr.sum(axis=1)                           # sum over every j < k
+    li = log[np.where(i[:, None] == i[None, :], 1, i[:, None] ^ i[None, :])]
+    li[i, i] = 0                                   # skip j == i
+    den = li.sum(axis=1)
+    E[k:] = exp[(tot[:, None] - lr - den[None, :]) % 255]
+    return E
+
+
+def test_encode_matrix_lagrange_closed_form_every_k():
+    """E's rows do not depend on m, so E(k, 256-k) covers every (k, m) with k+m <= 256.
+    Checked for every k against the C oracle, and for k <= 24 against the numpy oracle
+    (pure-Python Gauss-Jordan)."""
+    exp, log = _independent_log_exp()
+    for k in range(1, 256):
+        want = _lagrange_matrix(k, exp, log)
+        assert (cref.encode_matrix(k, 256 - k).astype(np.int64) == want).all(), k
+        if k <= 24:
+            assert (np.array(o.encode_matrix(k, 256 - k)) == want).all(), k
+
+
+def test_product_encode_matrix_lagrange_every_k(native_lib):
+    """The product's host matrix code (gf256.hpp via rs_encode_matrix, no device)."""
+    from callfs_amd.erasure import encode_matrix
+    exp, log = _independent_log_exp()
+    for k in range(1, 256):
+        assert (encode_matrix(k, 256 - k).astype(np.int64) == _lagrange_matrix(k, exp, log)).all(), k
