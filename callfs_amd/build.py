@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcallfs_rs.so")
 SOURCES = ["rs_kernels.hip", "sha256.hip", "rs_capi.cpp"]
-HEADERS = ["rs_kernels.hpp", "rs_apply.hpp", "tile_order.hpp", "gf256.hpp", "copy_pool.hpp", "sha256.hpp", os.path.join("..", "..", "include", "callfs_rs.h")]
+HEADERS = ["rs_kernels.hpp", "rs_apply.hpp", "tile_order.hpp", "gf256.hpp", "copy_pool.hpp", "dispatch.hpp", "sha256.hpp", os.path.join("..", "..", "include", "callfs_rs.h")]
 ARCH = os.environ.get("CALLFS_OFFLOAD_ARCH", "gfx950")
 
 

@@ -3,23 +3,22 @@
 // Replaces the SIMD kernels of github.com/klauspost/reedsolomon v1.13.3 (go.mod:13)
 // behind erasure/codec.go:36 (Encode), :55 (Reconstruct) and :59 (Verify).
 //
-// Design (DESIGN.md "Kernels"):
-//  * Byte-wise integer work, HBM-bound: no MFMA, no LDS. Each lane owns U 16-byte
-//    column vectors of a stripe and streams them through all K input shards with
-//    global_load_dwordx4, keeping the R output vectors in registers, then writes (or,
-//    for Verify rows, compares) them once: (K + R) * 16 bytes of compulsory HBM
-//    traffic per vector, nothing re-read (confirmed by rocprofv3 FETCH/WRITE_SIZE).
-//  * GF multiply by a wave-uniform coefficient c on 4 packed bytes = three v_perm_b32
-//    byte-selects from 8-byte tables: c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6]
-//    (gf256.hpp perm_tables). The three selectors depend only on the data word, so
-//    they are shared by all R rows; per row and data word the cost is 3 v_perm plus
-//    1.5 v_bitop3 (three-input XOR, gfx950). Tables and shard pointers are read
-//    through the constant address space, so they arrive by s_load in SGPRs: no LDS,
-//    no bank conflicts on random data, no per-lane table registers.
-//  * Input shards are consumed in pairs with the next pair's loads in flight, so
-//    register use does not grow with K (62 VGPRs at K=10, R=4: 8 waves/SIMD).
-//  * Ragged tails (S % 16) take the byte kernel. Shard pointers need no alignment: 16-B
-//    global accesses at any byte address are legal on gfx950 (rs_kernels.hpp).
+// Two kernels (DESIGN.md "Kernels"); launch_apply in rs_kernels.hip picks one per launch:
+//  * rs_apply_lds — every launch with k >= 4 inputs or R >= 5 rows (the bench's kernel).
+//    Per data byte, two LDS lookups into per-shard nibble tables return the products for
+//    all R rows at once. Table addresses are formed by v_perm_b32, and partial products
+//    are combined by v_bitop3 as a three-input XOR. The tables are staged into LDS once
+//    per block.
+//  * rs_apply_vec — k <= 3 with R <= 4. GF multiply by a wave-uniform coefficient c on 4
+//    packed bytes = three v_perm_b32 byte-selects from 8-byte tables:
+//    c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6] (gf256.hpp perm_tables). The tables arrive
+//    through the constant address space (s_load into SGPRs): no LDS.
+// Both stream each lane's 16-byte column vectors through all K input shards with
+// global_load_dwordx4 (non-temporal), keep the R outputs in registers and write (or,
+// for Verify rows, compare) them once: (K + R) * 16 bytes of compulsory HBM traffic per
+// vector, nothing re-read (rocprofv3 FETCH/WRITE_SIZE = algorithmic bytes).
+// Ragged tails (S % 16) take the byte kernel. Shard pointers need no alignment: 16-B
+// global accesses at any byte address are legal on gfx950 (rs_kernels.hpp).
 #pragma once
 
 #include <algorithm>
@@ -89,9 +88,13 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //            interleaved across 8/32/16/64 column segments of one stripe (LDS kernel: 0, 2..9)
 //   RING     LDS kernel input ring: 0 = three registers shifted each step (PD = 2);
 //            1 = PD+1 slots with the loop unrolled PD+1 times (static slot indices)
+//   NOMATH   measurement only (tools/kbench.hip): the LDS kernel with its lookups
+//            replaced by one XOR per input dword -- same loads, stores, grid and tile
+//            order -- i.e. the memory ceiling of a launch's traffic shape
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
-          int PD_ = 1, int ORD_ = 0, int RING_ = 0>
+          int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false>
 struct Policy {
+  static constexpr bool NOMATH = NOMATH_;
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
   static constexpr bool NT_LOAD = NT_LOAD_;
@@ -375,6 +378,14 @@ __device__ __forceinline__ uint32_t lds_row(const typename LdsAcc<RT>::T (&t)[4]
   return lo | hi;
 }
 
+// x in every dword of an accumulator element (NOMATH ceiling variant only).
+template <int RT>
+__device__ __forceinline__ typename LdsAcc<RT>::T lds_splat(uint32_t x) {
+  if constexpr (RT > 8) return typename LdsAcc<RT>::T{{x, x, x, x}};
+  else if constexpr (RT > 4) return (static_cast<uint64_t>(x) << 32) | x;
+  else return x;
+}
+
 template <int RT>
 __device__ __forceinline__ typename LdsAcc<RT>::T lds_zero() {
   if constexpr (RT > 8) return typename LdsAcc<RT>::T{{0, 0, 0, 0}};
@@ -431,7 +442,12 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll 1
       for (int i = 0; i < K; ++i) {
         if (i + 2 < K) x2 = ld(i + 2);
-        lds_mac<RT>(acc, x0, lds0 + static_cast<uint32_t>(i) * 32u * W);
+        if constexpr (P::NOMATH) {
+#pragma unroll
+          for (int w = 0; w < 4; ++w) acc[w][0] = acc[w][0] ^ lds_splat<RT>(word(x0, w));
+        } else {
+          lds_mac<RT>(acc, x0, lds0 + static_cast<uint32_t>(i) * 32u * W);
+        }
         x0 = x1;
         x1 = x2;
       }
@@ -448,7 +464,12 @@ void rs_apply_lds(ApplyArgs a) {
           const int i = i0 + s;
           if (i < K) {
             if (i + PD < K) xr[(s + PD) % NR] = ld(i + PD);
-            lds_mac<RT>(acc, xr[s], lds0 + static_cast<uint32_t>(i) * 32u * W);
+            if constexpr (P::NOMATH) {
+#pragma unroll
+              for (int w = 0; w < 4; ++w) acc[w][0] = acc[w][0] ^ lds_splat<RT>(word(xr[s], w));
+            } else {
+              lds_mac<RT>(acc, xr[s], lds0 + static_cast<uint32_t>(i) * 32u * W);
+            }
           }
         }
       }

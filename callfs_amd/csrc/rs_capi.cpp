@@ -30,6 +30,7 @@
 
 #include "../../include/callfs_rs.h"
 #include "copy_pool.hpp"
+#include "dispatch.hpp"
 #include "gf256.hpp"
 #include "rs_kernels.hpp"
 #include "sha256.hpp"
@@ -521,22 +522,18 @@ int run_on(rs_ctx* ctx, Device* dev, const std::shared_ptr<const Tables>& tp, si
   return rc;
 }
 
-// Ways to split one large object's columns over (device, lane) pairs: every output
-// byte depends only on the same column of the inputs, so column ranges are independent
-// (the in-process form of bench.py's column_slices). Objects of at least
-// CALLFS_RS_SPLIT_MIN_BYTES over all n shards (default 256 MiB) are split
-// CALLFS_RS_SPLIT_WAYS ways (default: one per device), each way on its own lane, so a
-// multi-GPU host moves one object over every GPU's PCIe link at once.
+// Ways to split one large object's columns over (device, lane) pairs (dispatch.hpp):
+// objects of at least CALLFS_RS_SPLIT_MIN_BYTES over all n shards (default 256 MiB)
+// are split CALLFS_RS_SPLIT_WAYS ways (default: one per device), each way on its own
+// lane, so a multi-GPU host moves one object over every GPU's PCIe link at once.
 int split_ways(const rs_ctx* ctx, size_t S, int n, int batch) {
-  if (batch != 1) return 1;
+  // read per call (cheap next to a >= 256 MiB object; tests change them in-process)
   const char* e = std::getenv("CALLFS_RS_SPLIT_MIN_BYTES");
   const unsigned long long min_bytes = e ? std::strtoull(e, nullptr, 0) : (256ull << 20);
-  if (static_cast<unsigned long long>(S) * n < min_bytes) return 1;
   const char* w = std::getenv("CALLFS_RS_SPLIT_WAYS");
-  int ways = w ? std::atoi(w) : static_cast<int>(ctx->devs.size());
-  ways = std::max(1, std::min(ways, static_cast<int>(ctx->devs.size()) * kMaxLanesPerDevice));
-  // at least 4 MiB of columns per way
-  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(ways, S >> 22)));
+  const int ways_req = w ? std::atoi(w) : 0;
+  return callfs::split_ways(ctx->devs.size(), kMaxLanesPerDevice, S, n, batch, min_bytes,
+                            ways_req);
 }
 
 template <class InF, class OutF>
@@ -548,19 +545,16 @@ int run_host(rs_ctx* ctx, const std::shared_ptr<const Tables>& tp, size_t S, int
   const unsigned base = ctx->rr.fetch_add(1);
   const int ways = split_ways(ctx, S, tp->k + tp->m, batch);
   if (ways == 1)
-    return run_on(ctx, ctx->devs[base % nd].get(), tp, S, batch, host_in, host_out,
-                  stripe_status, join, 0);
-  // column parts [c[p], c[p+1]), 4 KiB aligned
-  std::vector<size_t> c(ways + 1, 0);
-  for (int p = 1; p < ways; ++p) c[p] = std::min(S, round_up(S / ways * p, 4096));
-  c[ways] = S;
+    return run_on(ctx, ctx->devs[device_slot(base, 0, nd)].get(), tp, S, batch, host_in,
+                  host_out, stripe_status, join, 0);
+  const std::vector<size_t> c = column_parts(S, ways);  // parts [c[p], c[p+1])
   std::vector<int> rc(ways, RS_OK), flag(ways, 0);
   std::vector<std::thread> th;
   for (int p = 0; p < ways; ++p)
     th.emplace_back([&, p] {
       const size_t c0 = c[p];
       if (c[p + 1] <= c0) return;
-      rc[p] = run_on(ctx, ctx->devs[(base + p) % nd].get(), tp, c[p + 1] - c0, 1,
+      rc[p] = run_on(ctx, ctx->devs[device_slot(base, p, nd)].get(), tp, c[p + 1] - c0, 1,
                      [&](int b, int i) { return host_in(b, i) + c0; },
                      [&](int b, int i) { return host_out(b, i) + c0; }, &flag[p], join, c0);
     });
@@ -899,8 +893,7 @@ int rs_init(rs_ctx** out, unsigned device_mask) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RS_E_HIP;
   auto ctx = std::make_unique<rs_ctx>();
-  for (int d = 0; d < count && d < 32; ++d) {
-    if (device_mask && !((device_mask >> d) & 1u)) continue;
+  for (int d : select_devices(count, device_mask)) {
     auto dev = std::make_unique<Device>();
     dev->id = d;
     ctx->devs.push_back(std::move(dev));

@@ -3,6 +3,7 @@
 // on MI355X (DESIGN.md "Kernel tuning log").
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <string>
@@ -67,20 +68,30 @@ int tile_order_override() {
 // Tiles per kernel launch. Blocks are dealt to the 8 XCDs round-robin and each XCD runs
 // its share in order, so over a long grid the XCDs drift apart and the tiles in flight
 // spread over more of the address space than the tile order intends. Grids of more than
-// twice about 2 GiB of shard traffic are cut into equal consecutive slices of at most
-// that much (one launch each, same tile order), which resets the drift
-// (tools/slice_tiles_sweep.sh, % of 8 TB/s, unsliced -> sliced: RS(10,4) 64 MiB objects
-// x 256 72.8 -> 75.6-75.8, 1 MiB x 1,024 75.9 -> 76.7-77.3, 1 GiB objects x 8 74.7 ->
-// 75.3-76.0, RS(4,2) 1 MiB x 2,048 75.4 -> 76.0-76.4; the bench grid, 3.5 GiB, stays
-// whole). CALLFS_RS_MAX_TILES_PER_LAUNCH sets the slice in tiles instead.
+// twice about 4 GiB of shard traffic are cut into equal consecutive slices of at most
+// that much (one launch each, same tile order), which resets the drift. Round 2 sweep
+// (tools/slice_rule_sweep.sh, profiles/r02/slice_rule/, % of 8 TB/s, unsliced / 2 GiB /
+// 4 GiB slices): RS(10,4) 64 MiB objects x 256 (24 GiB) 73.1 / 77.5 / 77.4, 1 MiB x 1,024
+// 77.9 / 79.2 / 79.4, RS(4,2) 1 MiB x 2,048 76.8 / 79.2 / 79.3: long memory-bound grids
+// need slices, and 4 GiB ones keep the gain. Every slice boundary drains the machine,
+// which costs the grids of 4.5-12 GiB that 2 GiB slices used to cut: RS(10,8) 73.9 / 73.4
+// / 74.0, RS(10,16) 69.3 / 68.0 / 69.2 (unsliced at 4 GiB), RS(20,4) 77.4 / 75.9 / 75.8
+// (unsliced at 4 GiB), RS(32,8) 70.1 / 68.4 / 69.6, RS(32,16) 56.0 / 54.6 / 55.8; the
+// bench grid (3.5 GiB) stays whole either way. CALLFS_RS_MAX_TILES_PER_LAUNCH sets the
+// slice in tiles instead.
+std::atomic<long long> g_slice_tiles_override{-1};
+
 uint32_t slice_tiles(int streams) {
   static const long forced = [] {
     const char* e = std::getenv("CALLFS_RS_MAX_TILES_PER_LAUNCH");
     return e ? std::atol(e) : 0L;
   }();
+  const long long ov = g_slice_tiles_override.load(std::memory_order_relaxed);
+  if (ov == 0) return ~0u;  // never slice
+  if (ov > 0) return static_cast<uint32_t>(std::min<long long>(std::max<long long>(ov, 1024), 1LL << 30));
   if (forced >= 1024) return static_cast<uint32_t>(std::min<long>(forced, 1L << 30));
   const uint64_t tile_bytes = 8192ull * static_cast<uint64_t>(std::max(1, streams));
-  return static_cast<uint32_t>(std::max<uint64_t>(4096, (2ull << 30) / tile_bytes));
+  return static_cast<uint32_t>(std::max<uint64_t>(4096, (4ull << 30) / tile_bytes));
 }
 
 // Launches `grid` blocks of one kernel as consecutive slices (see slice_tiles). Launches
@@ -92,7 +103,7 @@ void launch_sliced(uint32_t grid, int streams, ApplyArgs& a, Launch&& launch) {
   const uint32_t all_rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
   const bool read_only = (a.verify_mask & all_rows) == all_rows;
   const uint32_t lim = read_only ? grid : slice_tiles(streams);
-  const uint32_t nsl = grid > 2 * lim ? (grid + lim - 1) / lim : 1;
+  const uint32_t nsl = grid / 2 > lim ? (grid + lim - 1) / lim : 1;
   const uint32_t per = (grid + nsl - 1) / nsl;
   for (uint32_t t0 = 0; t0 < grid; t0 += per) {
     a.t_base = t0;
@@ -147,6 +158,10 @@ const auto kLdsWideQ8 = lds_wide_table<LdsWideQ8Policy>(std::make_integer_sequen
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
 }  // namespace
+
+void set_slice_tiles_for_tuning(long long tiles) {
+  g_slice_tiles_override.store(tiles, std::memory_order_relaxed);
+}
 
 hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)

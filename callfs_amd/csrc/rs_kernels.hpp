@@ -55,4 +55,9 @@ inline int shard_addr_tz(const void* const* p, int count) {
 // Returns hipSuccess or the launch error.
 hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false);
 
+// Tuning hook for tools/kbench.hip (not part of the C ABI): tiles per launch slice for
+// every later launch_apply in the process; 0 = never slice, < 0 = the built-in rule
+// (CALLFS_RS_MAX_TILES_PER_LAUNCH or ~4 GiB of traffic per slice).
+void set_slice_tiles_for_tuning(long long tiles);
+
 }  // namespace callfs

@@ -7,6 +7,8 @@
 //  4. CopyPool under concurrent callers
 //  5. tile orders (tile_order.hpp): every block -> (stripe, tile) map is a bijection, and
 //     the launch rules pick the measured orders for known layouts
+//  6. multi-device placement (dispatch.hpp) over mocked device lists: mask selection,
+//     round-robin device slots, split ways and column part boundaries
 #include <cstdio>
 #include <random>
 #include <cstring>
@@ -14,6 +16,7 @@
 #include <vector>
 
 #include "copy_pool.hpp"
+#include "dispatch.hpp"
 #include "gf256.hpp"
 #include "tile_order.hpp"
 
@@ -256,6 +259,52 @@ int main() {
     CHECK(vec_tile_order(349526, tps_of(349526), 8) == TileOrder::kGroup2);
     CHECK(vec_tile_order(16 * MiB, tps_of(16 * MiB), 24) == TileOrder::kSeg16);
     CHECK(vec_tile_order(107374183, tps_of(107374183), 8) == TileOrder::kConsecutive);
+  }
+  // 6. multi-device placement (dispatch.hpp), mocked device counts
+  {
+    // rs_init's mask: 0 = all, bit d = device d, bits beyond the visible count ignored
+    CHECK((select_devices(8, 0) == std::vector<int>{0, 1, 2, 3, 4, 5, 6, 7}));
+    CHECK((select_devices(8, 0x81u) == std::vector<int>{0, 7}));
+    CHECK((select_devices(2, 0xFCu).empty()));
+    CHECK((select_devices(40, 0).size() == 32));
+    CHECK((select_devices(1, 1u) == std::vector<int>{0}));
+    // round robin: consecutive tickets walk the devices; parts of one call start at the
+    // call's device and take consecutive ones
+    for (size_t nd : {1u, 2u, 3u, 8u}) {
+      std::vector<int> hits(nd, 0);
+      for (unsigned t = 0; t < 8 * nd; ++t) hits[device_slot(t, 0, nd)]++;
+      for (size_t d = 0; d < nd; ++d) CHECK(hits[d] == 8);
+      for (int p = 0; p < 8; ++p) CHECK(device_slot(5, p, nd) == (5 + static_cast<size_t>(p)) % nd);
+    }
+    CHECK(device_slot(~0u, 1, 8) == (static_cast<size_t>(~0u) + 1) % 8);  // ticket wrap
+    // split ways: single-stripe calls of >= min bytes, one way per device by default,
+    // capped by lanes and by 4 MiB of columns per way
+    const unsigned long long min_b = 256ull << 20;
+    const size_t S1g = 107374183;  // 1 GiB RS(10,4)
+    CHECK(split_ways(8, 8, S1g, 14, 1, min_b, 0) == 8);
+    CHECK(split_ways(1, 8, S1g, 14, 1, min_b, 0) == 1);
+    CHECK(split_ways(8, 8, S1g, 14, 2, min_b, 0) == 1);          // batches never split
+    CHECK(split_ways(8, 8, 1 << 20, 14, 1, min_b, 0) == 1);      // 14 MiB < 256 MiB
+    CHECK(split_ways(2, 8, S1g, 14, 1, min_b, 5) == 5);          // explicit ways
+    CHECK(split_ways(1, 8, S1g, 14, 1, min_b, 100) == 8);        // lane cap
+    CHECK(split_ways(8, 8, 20u << 20, 14, 1, 1u << 20, 64) == 5);  // 4 MiB per way
+    CHECK(split_ways(0, 8, S1g, 14, 1, min_b, 0) == 1);
+    // column parts: cover [0, S) exactly, interior boundaries 4 KiB aligned, in order
+    for (size_t S : {S1g, static_cast<size_t>(13000002), static_cast<size_t>(4096 * 8 + 5)})
+      for (int w : {1, 2, 3, 5, 8}) {
+        const std::vector<size_t> c = column_parts(S, w);
+        CHECK(c.size() == static_cast<size_t>(w) + 1 && c.front() == 0 && c.back() == S);
+        for (int p = 1; p <= w; ++p) CHECK(c[p] >= c[p - 1]);
+        for (int p = 1; p < w; ++p) CHECK(c[p] % 4096 == 0 || c[p] == S);
+      }
+    // the 8-way split of a 1 GiB object over 8 devices: one part per device, each a
+    // nonempty column range of about S/8
+    const std::vector<size_t> c8 = column_parts(S1g, 8);
+    for (int p = 0; p < 8; ++p) {
+      const size_t w = c8[p + 1] - c8[p];
+      CHECK(w > 0 && w <= S1g / 8 + 4096);
+      CHECK(device_slot(0, p, 8) == static_cast<size_t>(p));
+    }
   }
   std::printf(fails ? "FAILED %d\n" : "host_test ok\n", fails);
   return fails ? 1 : 0;

@@ -959,3 +959,44 @@ def test_pinned_mixed_with_pageable_uses_staging(native_lib):
         assert np.array_equal(np.frombuffer(par[j], np.uint8), want[j])
     assert N.lib.rs_host_free(ctx.handle, ctypes.c_void_p(src.ptr + 1)) == N.RS_E_ARG
     src.close()
+
+
+# ---- configs[3]: per-rank byte-column slices of 1 GiB objects -------------------------
+
+@pytest.mark.parametrize("world", [8, 3])
+def test_configs3_rank_column_slices_reassemble(native_lib, world):
+    """BASELINE configs[3] as bench.py --object-bytes runs it on `world` GPUs, every rank
+    here on cuda:0: rank r holds columns column_slices(S, world)[r] of all k data shards of
+    a 1 GiB RS(10,4) object (S = 107,374,183) in its own StripeBatch, encodes, then decodes
+    erase {0,1,2,3} through Plan. The slices reassembled are the whole object's parity and
+    reconstruction: compared with the C oracle over the full 1 GiB (16 threads)."""
+    import torch
+    from callfs_amd.device import Plan, StripeBatch
+    from callfs_amd.sharding import column_slices
+    k, m, S = 10, 4, 107_374_183
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC0F3)
+    data = torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g)
+    parity = torch.empty((m, S), dtype=torch.uint8, device=dev)
+    present = [i not in (0, 1, 2, 3) for i in range(k + m)]
+    for off, w in column_slices(S, world):
+        if not w:
+            continue
+        sb = StripeBatch(k, m, w, 1, dev)
+        sb.buf[0, :k, :w].copy_(data[:, off:off + w])
+        Plan.for_batch(sb).launch()
+        parity[:, off:off + w].copy_(sb.buf[0, k:, :w])
+        keep = sb.buf[0, :4, :w].clone()
+        sb.buf[0, :4, :w].zero_()
+        dec = Plan.for_batch(sb, present=present)
+        dec.launch()
+        assert not dec.corrupt()
+        assert torch.equal(sb.buf[0, :4, :w], keep), (off, w)
+        del sb, keep
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    want = cref.encode([host[i] for i in range(k)], k, m, simd=True, nthreads=16)
+    got = parity.cpu().numpy()
+    for j in range(m):
+        assert np.array_equal(got[j], want[j]), j

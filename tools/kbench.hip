@@ -246,6 +246,21 @@ int main(int argc, char** argv) {
   vs.push_back(Variant{"prod dispatch", [](const ApplyArgs& a, hipStream_t s) {
                          CK(launch_apply(a, s));
                        }});
+  if (std::getenv("KB_SLICE")) {  // the production dispatch at other launch-slice sizes
+    static const int streams = k + m;
+    auto sliced = [](const char* name, double gib) {
+      return Variant{name, [gib](const ApplyArgs& a, hipStream_t s) {
+                       set_slice_tiles_for_tuning(
+                           gib <= 0 ? 0 : static_cast<long long>(gib * (1ull << 30) / (8192.0 * streams)));
+                       CK(launch_apply(a, s));
+                       set_slice_tiles_for_tuning(-1);
+                     }};
+    };
+    vs.push_back(sliced("prod slice none", 0));
+    vs.push_back(sliced("prod slice 1GiB", 1));
+    vs.push_back(sliced("prod slice 4GiB", 4));
+    vs.push_back(sliced("prod slice 8GiB", 8));
+  }
   if (const char* sp = std::getenv("KB_SPLIT")) {  // same work as launches over B/N stripes each
     static const int parts = std::max(1, std::atoi(sp));
     vs.push_back(Variant{"prod split", [](const ApplyArgs& a, hipStream_t s) {
@@ -392,6 +407,20 @@ int main(int argc, char** argv) {
       case 12: KB_RINGS(12) break;
       case 16: KB_RINGS(16) break;
     }
+  }
+  {  // memory ceiling of this traffic shape: the LDS kernel's loads/stores/grid, no lookups
+    static void (*const nomath_g2[16])(const ApplyArgs&, hipStream_t) = {
+#define KB_NM(R) [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, Policy<2, 1, true, true, false, 512, (R > 8 ? 4 : 2), 5, (R > 8 ? 1 : 0), true>>(a, s); }
+        KB_NM(1), KB_NM(2), KB_NM(3), KB_NM(4), KB_NM(5), KB_NM(6), KB_NM(7), KB_NM(8),
+        KB_NM(9), KB_NM(10), KB_NM(11), KB_NM(12), KB_NM(13), KB_NM(14), KB_NM(15), KB_NM(16)};
+#undef KB_NM
+    static void (*const nomath_c[16])(const ApplyArgs&, hipStream_t) = {
+#define KB_NM(R) [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, Policy<2, 1, true, true, false, 512, (R > 8 ? 4 : 2), 0, (R > 8 ? 1 : 0), true>>(a, s); }
+        KB_NM(1), KB_NM(2), KB_NM(3), KB_NM(4), KB_NM(5), KB_NM(6), KB_NM(7), KB_NM(8),
+        KB_NM(9), KB_NM(10), KB_NM(11), KB_NM(12), KB_NM(13), KB_NM(14), KB_NM(15), KB_NM(16)};
+#undef KB_NM
+    vs.push_back(Variant{"nomath g2 (ceiling)", [m](const ApplyArgs& a, hipStream_t s) { nomath_g2[m - 1](a, s); }, false});
+    vs.push_back(Variant{"nomath consec (ceiling)", [m](const ApplyArgs& a, hipStream_t s) { nomath_c[m - 1](a, s); }, false});
   }
   if (rs10_4) vs.push_back(Variant{"read-only 10 streams (bytes: 10/14)", [](const ApplyArgs& a, hipStream_t s) {
                          const unsigned g = static_cast<unsigned>((a.nvec + 511) / 512 * a.batch);

@@ -53,7 +53,7 @@ def main(src, dst, k=10, m=4, S=1 << 20, B=256, erase=(0, 1, 2, 3), kernel="rs_a
         fetch = statistics.median(pmc["FETCH_SIZE"][idx])
         write = statistics.median(pmc["WRITE_SIZE"][idx])
         fetch_b, write_b = fetch * 1024 * 2, write * 1024
-        # grids of > 2 x ~2 GiB of traffic run as several dispatches per plan launch
+        # grids of > 2 x ~4 GiB of traffic run as several dispatches per plan launch
         # (rs_kernels.hip slice_tiles): scale per-dispatch counters to one launch
         slices = max(1, round(algo / (fetch_b + write_b)))
         avg = sum(ds) / len(ds) * slices
