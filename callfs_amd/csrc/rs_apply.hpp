@@ -91,10 +91,17 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //   NOMATH   measurement only (tools/kbench.hip): the LDS kernel with its lookups
 //            replaced by one XOR per input dword -- same loads, stores, grid and tile
 //            order -- i.e. the memory ceiling of a launch's traffic shape
+//   REALIGN  LDS kernel, RING 0: input shards whose base is not 16-B aligned are read
+//            with aligned 16-B loads and realigned in registers (neighbour lane's
+//            vector by DPP wave_shl:1, v_alignbyte funnel shift) instead of unaligned
+//            global_load_dwordx4
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
-          int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false>
+          int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, bool REALIGN_ = false>
 struct Policy {
   static constexpr bool NOMATH = NOMATH_;
+  static constexpr bool REALIGN = REALIGN_;
+  // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads
+  static constexpr int TILE_VECS = REALIGN_ ? BS_ / 64 * 63 : BS_ * U_;
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
   static constexpr bool NT_LOAD = NT_LOAD_;
@@ -261,6 +268,58 @@ void rs_apply_vec(ApplyArgs a) {
   }
 }
 
+// ---- realigned loads of misaligned shards (Policy::REALIGN) ----------------------------
+// A shard at p with d = p & 15: vector v (bytes [16v, 16v+16) of p) lies in the aligned
+// vectors A[v] = (p-d)[v] and A[v+1]. A REALIGN wave loads 64 consecutive aligned vectors
+// A[w0 .. w0+63], one per lane, and produces the 63 vectors w0 .. w0+62: lane l takes
+// A[l+1] from lane l+1 by DPP wave_shl:1 and funnel-shifts the pair by d bytes
+// (v_alignbyte). Lane 63 only loads. Each lane issues one aligned global_load_dwordx4
+// per shard, as the unaligned kernel does, and every realigned byte comes from the wave's
+// own loads. The next wave reloads its first vector, 1/64 of the lines, from cache.
+// Load addresses are clamped to A[nvec] (d > 0) or A[nvec-1] (d = 0). Every aligned
+// vector up to A[nvec] contains a byte of the shard (A[nvec] starts at
+// p + 16*nvec - d <= p + S - 1). An aligned 16-B block never straddles a page, so no
+// load can fault outside the shard's pages. (Two vector loads per shard, A[v] and A[v+1],
+// measured 9-13 points slower, and a per-lane tail load or a scalar tail load cost
+// waits: these kernels are sensitive to the count of memory instructions, not only to
+// HBM bytes.)
+template <int Q>
+__device__ __forceinline__ uint4 funnel16(const uint4& A, const uint4& B, uint32_t r) {
+  const uint32_t s[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+  return make_uint4(__builtin_amdgcn_alignbyte(s[Q + 1], s[Q], r),
+                    __builtin_amdgcn_alignbyte(s[Q + 2], s[Q + 1], r),
+                    __builtin_amdgcn_alignbyte(s[Q + 3], s[Q + 2], r),
+                    __builtin_amdgcn_alignbyte(s[Q + 4], s[Q + 3], r));
+}
+
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x130, 0xf, 0xf, false));
+}
+
+// Aligned load of A[v] of shard p (v clamped as above); nvec >= 1.
+template <class P>
+__device__ __forceinline__ uint4 ld_aligned(const uint8_t* p, uint64_t v, uint64_t nvec) {
+  const uint32_t d = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u;
+  const uint64_t vmax = d ? nvec : nvec - 1;
+  return load16<P>(reinterpret_cast<const uint4*>(p - d) + (v < vmax ? v : vmax));
+}
+
+// Vector v of shard p from this lane's aligned A[v] and the next lane's A[v+1]; every
+// lane of the wave executes this (lane 63's result is not used).
+__device__ __forceinline__ uint4 realign(const uint8_t* p, const uint4& A) {
+  const uint32_t d = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u;
+  if (d == 0) return A;  // wave-uniform
+  const uint4 B = make_uint4(from_next_lane(A.x), from_next_lane(A.y), from_next_lane(A.z),
+                             from_next_lane(A.w));
+  const uint32_t r = d & 3u;
+  switch (d >> 2) {  // wave-uniform
+    case 0: return funnel16<0>(A, B, r);
+    case 1: return funnel16<1>(A, B, r);
+    case 2: return funnel16<2>(A, B, r);
+    default: return funnel16<3>(A, B, r);
+  }
+}
+
 // ---- LDS nibble-table variant ---------------------------------------------------------
 // Per data byte two LDS lookups (low / high nibble) return the products for all RT rows
 // at once (ds_read_b32 / b64 / b128 for RT <= 4 / 8 / 16), so the cost per data dword
@@ -417,7 +476,8 @@ void rs_apply_lds(ApplyArgs a) {
   // absolute LDS address of the tables (0 unless static LDS is ever added)
   const uint32_t lds0 = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)smem));
-  const uint32_t tps = static_cast<uint32_t>((a.nvec + BS - 1) / BS);
+  constexpr int TV = P::TILE_VECS;
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + TV - 1) / TV);
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
   // one tile per block (vec_grid), or (PERSIST) grid-stride over tiles so that the
   // table prologue is paid once per block; either way the blocks in flight cover a
@@ -425,8 +485,13 @@ void rs_apply_lds(ApplyArgs a) {
   for (uint32_t t = a.t_base + blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
     uint32_t stripe, tile;
     map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
-    const uint64_t v0 = static_cast<uint64_t>(tile) * BS + threadIdx.x;
-    if (v0 >= a.nvec) continue;
+    // REALIGN: wave w of the tile produces vectors tile*TV + 63w + lane (lanes 0..62)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t v0 = P::REALIGN ? static_cast<uint64_t>(tile) * TV + (threadIdx.x >> 6) * 63u + lane
+                                   : static_cast<uint64_t>(tile) * BS + threadIdx.x;
+    // lanes that store (REALIGN: lane 63 and lanes past the shard only load)
+    const bool active = v0 < a.nvec && (!P::REALIGN || lane != 63u);
+    if (P::REALIGN ? (v0 - lane >= a.nvec) : !active) continue;  // REALIGN: whole wave idle
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
     auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
@@ -436,7 +501,19 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[w][j] = lds_zero<RT>();
 
-    if constexpr (P::RING == 0) {
+    if constexpr (P::REALIGN) {
+      static_assert(!P::NOMATH, "REALIGN: no NOMATH form");
+      // ring of three aligned vectors, realigned when consumed
+      auto lda = [&](int i) { return ld_aligned<P>(in[i], v0, a.nvec); };
+      uint4 x0 = lda(0), x1 = K > 1 ? lda(1) : x0, x2 = x0;
+#pragma unroll 1
+      for (int i = 0; i < K; ++i) {
+        if (i + 2 < K) x2 = lda(i + 2);
+        lds_mac<RT>(acc, realign(in[i], x0), lds0 + static_cast<uint32_t>(i) * 32u * W);
+        x0 = x1;
+        x1 = x2;
+      }
+    } else if constexpr (P::RING == 0) {
       // ring of three shard vectors: shard i is consumed while i+1, i+2 load
       uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = x0;
 #pragma unroll 1
@@ -482,6 +559,7 @@ void rs_apply_lds(ApplyArgs a) {
       const uint4 o = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
                                  lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
       uint4* dst = reinterpret_cast<uint4*>(out[r]) + v0;
+      if (P::REALIGN && !active) continue;
       if ((a.verify_mask >> r) & 1u) {
         const uint4 y = *dst;
         bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) != 0;
@@ -529,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_bytes(ApplyArgs a, uint64_t b
 // `blocks_per_cu` blocks on each of the 256 CUs.
 template <class P>
 inline unsigned vec_grid(uint64_t nvec, int batch, int blocks_per_cu = 8) {
-  const uint64_t tile = static_cast<uint64_t>(P::BS) * P::U;
+  const uint64_t tile = static_cast<uint64_t>(P::TILE_VECS);
   const uint64_t ntiles = (nvec + tile - 1) / tile * static_cast<uint64_t>(batch);
   if (P::PERSIST) return static_cast<unsigned>(std::min<uint64_t>(ntiles, 256ull * blocks_per_cu));
   return static_cast<unsigned>(ntiles);

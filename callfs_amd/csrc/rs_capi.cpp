@@ -202,6 +202,7 @@ struct HostBuf {
 struct LayoutHint {
   int addr_tz = 0;
   uint64_t stripe_stride = 0;
+  uint32_t in_misalign = 0;
 };
 
 // One pipeline stage of the host-memory path: a stream, a pinned chunk buffer and its
@@ -289,8 +290,13 @@ template <class F>
 LayoutHint fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
   std::memset(h + L.status_off, 0, sizeof(int) * static_cast<size_t>(batch));
   auto* in = reinterpret_cast<const uint8_t**>(h + L.in_off);
+  uint32_t misalign = 0;
   for (int b = 0; b < batch; ++b)
-    for (int i = 0; i < t.k; ++i) in[static_cast<size_t>(b) * t.k + i] = shard_ptr(b, t.valid[i]);
+    for (int i = 0; i < t.k; ++i) {
+      const uint8_t* p = shard_ptr(b, t.valid[i]);
+      in[static_cast<size_t>(b) * t.k + i] = p;
+      misalign |= static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u;
+    }
   for (size_t gi = 0; gi < t.groups.size(); ++gi) {
     const Group& g = t.groups[gi];
     auto* out = reinterpret_cast<uint8_t**>(h + L.out_off[gi]);
@@ -305,6 +311,7 @@ LayoutHint fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h
   for (const Group& g : t.groups)
     for (int i : g.shard) s0.push_back(shard_ptr(0, i));
   LayoutHint hint;
+  hint.in_misalign = misalign;
   hint.addr_tz = shard_addr_tz(s0.data(), static_cast<int>(s0.size()));
   if (batch > 1) {
     const int v = t.valid[0];
@@ -335,6 +342,7 @@ hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_
     a.batch = batch;
     a.addr_tz = hint.addr_tz;
     a.stripe_stride = hint.stripe_stride;
+    a.in_misalign = hint.in_misalign;
     hipError_t e = launch_apply(a, s);
     if (e != hipSuccess) return e;
   }
@@ -362,6 +370,12 @@ class PinnedRegistry {
     std::lock_guard<std::mutex> g(mu_);
     return ranges_.erase(reinterpret_cast<uintptr_t>(p)) == 1;
   }
+  // size of the allocation starting at p (0 when p is not one)
+  size_t size_of(void* p) const {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = ranges_.find(reinterpret_cast<uintptr_t>(p));
+    return it == ranges_.end() ? 0 : it->second;
+  }
   // true when [p, p+n) lies inside one registered allocation
   bool contains(const void* p, size_t n) const {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -387,15 +401,84 @@ class PinnedRegistry {
   std::map<uintptr_t, size_t> ranges_;
 };
 
+// Idle rs_host_alloc buffers kept for reuse. Page-locking a fresh buffer costs about
+// 0.2 s per 384 MiB, so a server that allocates a pinned body per request and frees it
+// after the call ran 25-30x slower than one that reuses buffers (RS(4,2) 256 MiB,
+// zero-copy: 1.6 vs 48 GiB/s encode). rs_host_free parks a buffer here;
+// rs_host_alloc takes the smallest parked buffer that fits without wasting more than a
+// quarter of it. Parked bytes are capped by CALLFS_RS_HOST_POOL_BYTES (default 8 GiB;
+// 0 disables parking): beyond it the largest parked buffers are released.
+class HostPool {
+ public:
+  struct Buf {
+    void* p;
+    size_t cap;
+  };
+  // a parked buffer of at least n bytes, or {nullptr, 0}
+  Buf take(size_t n) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = idle_.lower_bound(n);
+    if (it == idle_.end() || it->first - n > it->first / 4) return {nullptr, 0};
+    Buf b{it->second, it->first};
+    idle_bytes_ -= it->first;
+    idle_.erase(it);
+    return b;
+  }
+  // park a buffer; returns the buffers to release now (over the cap)
+  std::vector<void*> put(void* p, size_t cap) {
+    std::vector<void*> drop;
+    std::lock_guard<std::mutex> g(mu_);
+    if (cap > limit()) {
+      drop.push_back(p);
+      return drop;
+    }
+    idle_.emplace(cap, p);
+    idle_bytes_ += cap;
+    while (idle_bytes_ > limit() && !idle_.empty()) {
+      auto last = std::prev(idle_.end());
+      idle_bytes_ -= last->first;
+      drop.push_back(last->second);
+      idle_.erase(last);
+    }
+    return drop;
+  }
+  std::vector<void*> drain() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<void*> all;
+    for (auto& kv : idle_) all.push_back(kv.second);
+    idle_.clear();
+    idle_bytes_ = 0;
+    return all;
+  }
+  size_t idle_bytes() {
+    std::lock_guard<std::mutex> g(mu_);
+    return idle_bytes_;
+  }
+
+ private:
+  static size_t limit() {
+    static const size_t v = [] {
+      const char* e = std::getenv("CALLFS_RS_HOST_POOL_BYTES");
+      return e ? static_cast<size_t>(std::strtoull(e, nullptr, 0)) : (8ull << 30);
+    }();
+    return v;
+  }
+  std::mutex mu_;
+  std::multimap<size_t, void*> idle_;
+  size_t idle_bytes_ = 0;
+};
+
 struct rs_ctx {
   std::vector<std::unique_ptr<Device>> devs;
   std::atomic<unsigned> rr{0};
   TableCache cache;
   CopyPool pool;
   PinnedRegistry pinned;
+  HostPool host_pool;
 
   ~rs_ctx() {
     for (void* p : pinned.all()) (void)hipHostFree(p);  // buffers the caller did not free
+    for (void* p : host_pool.drain()) (void)hipHostFree(p);
     for (auto& d : devs) {
       (void)hipSetDevice(d->id);
       for (auto& l : d->lanes) {
@@ -913,20 +996,29 @@ int rs_device_count(const rs_ctx* ctx) { return ctx ? static_cast<int>(ctx->devs
 int rs_host_alloc(rs_ctx* ctx, size_t bytes, void** out) {
   if (!ctx || !out || bytes == 0) return RS_E_ARG;
   *out = nullptr;
-  void* p = nullptr;
-  // portable: every device of the context may use it. Coherent: the kernels read and
-  // write it in place (zero-copy), and the caller refills the same buffer between calls,
-  // so device caches must not keep its lines across launches.
-  if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess)
-    return RS_E_NOMEM;
-  ctx->pinned.add(p, bytes);
-  *out = p;
+  HostPool::Buf b = ctx->host_pool.take(bytes);
+  if (!b.p) {
+    // 2 MiB granules: buffers freed by one request fit the next request of similar size
+    b.cap = round_up(bytes, 2u << 20);
+    // portable: every device of the context may use it. Coherent: the kernels read and
+    // write it in place (zero-copy), and the caller refills the same buffer between
+    // calls, so device caches must not keep its lines across launches.
+    if (hipHostMalloc(&b.p, b.cap, hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess)
+      return RS_E_NOMEM;
+  }
+  ctx->pinned.add(b.p, b.cap);
+  *out = b.p;
   return RS_OK;
 }
 
 int rs_host_free(rs_ctx* ctx, void* p) {
-  if (!ctx || !p || !ctx->pinned.remove(p)) return RS_E_ARG;
-  return hipHostFree(p) == hipSuccess ? RS_OK : RS_E_HIP;
+  if (!ctx || !p) return RS_E_ARG;
+  const size_t cap = ctx->pinned.size_of(p);
+  if (!cap || !ctx->pinned.remove(p)) return RS_E_ARG;
+  int rc = RS_OK;
+  for (void* q : ctx->host_pool.put(p, cap))
+    if (hipHostFree(q) != hipSuccess) rc = RS_E_HIP;
+  return rc;
 }
 
 int rs_shard_size(int k, int m, int64_t len, int64_t* shard_size) {

@@ -49,6 +49,15 @@ using LdsG8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 2>;
 using LdsG2Policy = dev::Policy<2, 1, true, true, false, 512, 2, 5>;
 using LdsQ8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 6>;
 using LdsQ16Policy = dev::Policy<2, 1, true, true, false, 512, 2, 8>;
+// Misaligned input shards with k >= 8 and R <= 8: aligned loads realigned in registers,
+// 63 vectors per wave, consecutive tiles (rs_apply.hpp REALIGN; tools/realign_sweep.sh,
+// profiles/r02/realign/, % of 8 TB/s, unaligned loads -> realigned): RS(10,4) 64 MiB
+// objects in the Split layout (S = 6,710,887) 66.5 -> 70.7, with aligned parity 68.5 ->
+// 72.7; RS(10,8) 1,048,577 B 63.6 -> 65.9; RS(16,4) 262,145 B 65.1 -> 66.2; RS(10,4)
+// 1,048,577 B 68.9 -> 69.8. With few inputs it loses (RS(4,2) 68.8 -> 67.4), and aligned
+// shards keep the plain kernel (the 504-vector tile costs 5 points there).
+using LdsRealignPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0, 0, false, true>;
+constexpr int kRealignMinK = 8;
 // CALLFS_RS_TILE_ORDER=consecutive|g8|g2|q8|q16 overrides the rule for every LDS-kernel
 // launch with R <= 8 (A/B on a deployment's own shard layout; unset = the rule).
 int tile_order_override() {
@@ -150,6 +159,7 @@ const auto kLdsG8 = lds_order_table<LdsG8Policy>(std::make_integer_sequence<int,
 const auto kLdsG2 = lds_order_table<LdsG2Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ8 = lds_order_table<LdsQ8Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ16 = lds_order_table<LdsQ16Policy>(std::make_integer_sequence<int, 8>{});
+const auto kLdsRealign = lds_order_table<LdsRealignPolicy>(std::make_integer_sequence<int, 8>{});
 template <class P, int... Rs>
 constexpr auto lds_wide_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 9, P>...};
@@ -203,9 +213,13 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         static_assert(LdsPolicy::BS == LdsWidePolicy::BS && LdsPolicy::U == LdsWidePolicy::U &&
                           LdsG8Policy::BS == LdsPolicy::BS && LdsG2Policy::BS == LdsPolicy::BS &&
                           LdsQ8Policy::BS == LdsPolicy::BS && LdsQ16Policy::BS == LdsPolicy::BS &&
-                          LdsWideQ8Policy::BS == LdsPolicy::BS,
+                          LdsWideQ8Policy::BS == LdsPolicy::BS && LdsRealignPolicy::BS == LdsPolicy::BS,
                       "one grid shape for every LDS policy");
-        const unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
+        unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
+        if (a.R <= 8 && a.in_misalign && a.K >= kRealignMinK) {
+          fn = kLdsRealign[a.R - 1];
+          gx = dev::vec_grid<LdsRealignPolicy>(a.nvec, a.batch);
+        }
         launch_sliced(gx, a.K + a.R, a, [&](uint32_t blocks) {
           hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, a);
         });

@@ -36,6 +36,10 @@ struct ApplyArgs {
   // first tile of this launch (launch_apply cuts grids of many tiles into consecutive
   // slices; a kernel's block b works on tile t_base + b of the whole tile order)
   uint32_t t_base;
+  // OR of (address & 15) over every input shard pointer of every stripe: nonzero when
+  // some input shard is not 16-B aligned (upstream Split layout of a contiguous object
+  // at odd S); selects the LDS kernel's realigning form (rs_apply.hpp REALIGN)
+  uint32_t in_misalign;
 };
 
 // addr_tz for a set of shard addresses: trailing zeros of the OR of their differences

@@ -1000,3 +1000,78 @@ def test_configs3_rank_column_slices_reassemble(native_lib, world):
     got = parity.cpu().numpy()
     for j in range(m):
         assert np.array_equal(got[j], want[j]), j
+
+
+def test_host_pool_reuses_freed_buffers(native_lib):
+    """rs_host_free parks a buffer and rs_host_alloc of a similar size gets it back (no new
+    page-locking per request); a parked pointer is no longer a valid rs_host_free argument;
+    a request much smaller than any parked buffer gets a new one; and a reused buffer with
+    stale contents still takes the zero-copy path correctly."""
+    import ctypes
+    from callfs_amd import _native as N
+    ctx = N.Context()
+    try:
+        k, m, S = 4, 2, 3 << 20
+        a = N.PinnedBuffer(k * S, ctx)
+        pa = a.ptr
+        a.array[:] = 0xEE
+        a.close()
+        assert N.lib.rs_host_free(ctx.handle, ctypes.c_void_p(pa)) == N.RS_E_ARG  # parked
+        b = N.PinnedBuffer(k * S - 4096, ctx)  # within a quarter: the parked buffer
+        assert b.ptr == pa
+        small = N.PinnedBuffer(4096, ctx)
+        assert small.ptr != pa
+        par = N.PinnedBuffer(m * S, ctx)
+        data = np.frombuffer(rnd(77, k * S), np.uint8)
+        b.array[: k * S - 4096] = data[: k * S - 4096]
+        view = np.ctypeslib.as_array((ctypes.c_uint8 * (k * S)).from_address(b.ptr))
+        view[k * S - 4096:] = data[k * S - 4096:]  # the rest of the reused 2 MiB granule
+        dp = (ctypes.c_void_p * k)(*[b.ptr + i * S for i in range(k)])
+        pp = (ctypes.c_void_p * m)(*[par.ptr + j * S for j in range(m)])
+        N.check(N.lib.rs_encode(ctx.handle, k, m, S, dp, pp))
+        want = cref.encode([data[i * S:(i + 1) * S] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(par.array[j * S:(j + 1) * S], want[j]), j
+        for buf in (b, small, par):
+            buf.close()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("k,m,S,batch,off", [
+    (10, 4, 17, 3, 1),                 # one vector per shard
+    (10, 4, 16 * 63 + 5, 4, 7),        # exactly one realigning wave's 63 vectors + tail
+    (10, 4, 16 * 64 + 9, 3, 2),        # 64 vectors: the second wave holds one
+    (12, 8, 4096 * 3 + 1, 5, 13),      # R = 8, odd stripe stride
+    (8, 2, 16 * 504 * 2 + 15, 2, 5),   # k = 8 (the rule's minimum), 504-vector tile boundaries
+    (10, 4, 1_000_003, 2, 11),         # Split layout of ~10 MB objects
+])
+def test_plan_misaligned_batch_realign(native_lib, k, m, S, batch, off):
+    """Contiguous stripes in the upstream Split layout at odd S (every input shard at its
+    own byte misalignment, odd stripe stride): k >= 8 launches take the realigning LDS
+    kernel (aligned loads, DPP + v_alignbyte, 63 vectors per wave). Encode, a decode
+    erasing m shards, and a decode with Verify rows, against the oracle per stripe."""
+    import torch
+    from callfs_amd.device import Plan
+    n = k + m
+    total = batch * n * S
+    buf = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device="cuda:0")
+    base = buf.data_ptr() + off
+    ptrs = [base + (b * n + i) * S for b in range(batch) for i in range(n)]
+    Plan(k, m, S, batch, ptrs).launch()
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()[off:off + total].copy()
+    for b in range(batch):
+        st = host[b * n * S:(b + 1) * n * S]
+        want = cref.encode([st[i * S:(i + 1) * S] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(st[(k + j) * S:(k + j + 1) * S], want[j]), (b, j)
+    for erase in (list(range(0, k, max(1, k // m)))[:m], [1, k]):  # m erasures / verify rows
+        for b in range(batch):
+            for i in erase:
+                s0 = off + (b * n + i) * S
+                buf[s0:s0 + S].zero_()
+        dec = Plan(k, m, S, batch, ptrs, present=[i not in erase for i in range(n)])
+        dec.launch()
+        assert not dec.corrupt(), erase
+        assert np.array_equal(buf.cpu().numpy()[off:off + total], host), erase

@@ -11,6 +11,12 @@
 // rs_reconstruct_batch (verify on) plus the per-object join copy.
 // CALLFS_E2E_PINNED=1: every buffer comes from rs_host_alloc (the server reading bodies
 // and shards into pinned memory), so calls take the zero-copy direct-DMA path.
+// Zero-copy concurrency probes:
+// CALLFS_E2E_EXTRA_PINNED_MIB=N: also hold N MiB of touched, unused rs_host_alloc memory
+//   (a larger pinned footprint without more concurrent calls);
+// CALLFS_E2E_SERIAL=1: one rs_* call at a time across all threads (concurrency without
+//   overlap: same footprint, calls serialised by a mutex in this harness);
+// CALLFS_E2E_FRESH=1: allocate (and free) the output buffers of every call anew.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -18,10 +24,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <random>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "callfs_rs.h"
@@ -46,6 +54,12 @@ struct MaybePinned {
     if (!g_pinned) ::operator delete(p);
     else rs_host_free(g_ctx, p);
   }
+  // default-initialise (no zero fill): a fresh per-call buffer costs what the server's
+  // allocation would, not a memset of the whole object
+  template <class U>
+  void construct(U* p) { ::new (static_cast<void*>(p)) U; }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
   template <class U>
   bool operator==(const MaybePinned<U>&) const { return true; }
   template <class U>
@@ -82,6 +96,23 @@ int main(int argc, char** argv) {
   g_ctx = ctx;
   g_pinned = std::getenv("CALLFS_E2E_PINNED") != nullptr;
   const size_t S = (L + k - 1) / k;
+  const bool serial = std::getenv("CALLFS_E2E_SERIAL") != nullptr;
+  const bool fresh = std::getenv("CALLFS_E2E_FRESH") != nullptr;
+  static std::mutex call_mu;
+  std::vector<void*> extra;  // 1 GiB pieces (one huge pinned allocation can fail)
+  if (const char* x = std::getenv("CALLFS_E2E_EXTRA_PINNED_MIB")) {
+    for (size_t left = std::strtoull(x, nullptr, 0) << 20; left;) {
+      const size_t piece = std::min<size_t>(left, 1ull << 30);
+      void* p = nullptr;
+      if (rs_host_alloc(ctx, piece, &p) != RS_OK) {
+        std::fprintf(stderr, "rs_host_alloc(%zu) failed\n", piece);
+        return 1;
+      }
+      for (size_t i = 0; i < piece; i += 4096) static_cast<uint8_t*>(p)[i] = static_cast<uint8_t>(i >> 12);
+      extra.push_back(p);
+      left -= piece;
+    }
+  }
   struct Thr {
     Bytes src, enc, out;
     std::vector<Bytes> sh;
@@ -122,6 +153,9 @@ int main(int argc, char** argv) {
         Bytes bjoin(nb > 0 ? L : 0);
         while (!stop.load(std::memory_order_relaxed)) {
           int rc;
+          std::unique_lock<std::mutex> serial_lock(call_mu, std::defer_lock);
+          if (serial) serial_lock.lock();
+          if (fresh) Bytes(n * S).swap(enc2);  // new pinned output buffer for this call
           if (nb > 0 && encode) {
             for (int b = 0; b < B; ++b) {
               for (int i = 0; i < k; ++i) bdata[static_cast<size_t>(b) * k + i] = me.enc.data() + S * i;
@@ -206,6 +240,7 @@ int main(int argc, char** argv) {
               k, m, L, T, nb > 0 ? nb : 1, erase.size(), e.first, d.first, e.second, d.second,
               bad ? "false" : "true");
   th_holder.reset();  // pinned buffers go back before the context
+  for (void* p : extra) rs_host_free(ctx, p);
   rs_shutdown(ctx);
   return bad ? 1 : 0;
 }

@@ -167,8 +167,18 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&buf, total));
   hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint32_t*>(buf),
                      total / 4, 12345u);
+  // KB_OUT_SEP=1: output rows in a separate buffer at a 256-B-aligned pitch (inputs keep
+  // `pitch`); KB_IN_SEP=1: input rows there instead (unaligned-shard A/B: which side
+  // pays for misaligned 16-B accesses)
+  const bool out_sep = std::getenv("KB_OUT_SEP") != nullptr, in_sep = std::getenv("KB_IN_SEP") != nullptr;
+  const size_t apitch = (S + 255) / 256 * 256;
+  const size_t opitch = out_sep ? apitch : pitch;
+  uint8_t* sep = nullptr;
+  if (out_sep || in_sep) CK(hipMalloc(&sep, apitch * (out_sep ? m : k) * B));
+  if (sep) hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint32_t*>(sep),
+                              apitch * (out_sep ? m : k) * B / 4, 777u);
   uint8_t* ref;  // parity of the production variant
-  CK(hipMalloc(&ref, pitch * m * B));
+  CK(hipMalloc(&ref, opitch * m * B));
 
   // tables (encode: parity rows of E)
   Mat E;
@@ -204,8 +214,12 @@ int main(int argc, char** argv) {
   parse(std::getenv("KB_IN"), islot);
   parse(std::getenv("KB_OUT"), oslot);
   for (int b = 0; b < B; ++b) {
-    for (int i = 0; i < k; ++i) in[b * k + i] = buf + (static_cast<size_t>(b) * n + islot[i]) * pitch;
-    for (int r = 0; r < m; ++r) out[b * m + r] = buf + (static_cast<size_t>(b) * n + oslot[r]) * pitch;
+    for (int i = 0; i < k; ++i)
+      in[b * k + i] = in_sep ? sep + (static_cast<size_t>(b) * k + i) * apitch
+                             : buf + (static_cast<size_t>(b) * n + islot[i]) * pitch;
+    for (int r = 0; r < m; ++r)
+      out[b * m + r] = out_sep ? sep + (static_cast<size_t>(b) * m + r) * apitch
+                               : buf + (static_cast<size_t>(b) * n + oslot[r]) * pitch;
   }
   void *d_in, *d_out, *d_tabs, *d_ltabs;
   int* d_status;
@@ -237,6 +251,8 @@ int main(int argc, char** argv) {
     s0.insert(s0.end(), out.begin(), out.begin() + m);
     a.addr_tz = shard_addr_tz(s0.data(), k + m);
     a.stripe_stride = B > 1 ? static_cast<uint64_t>(pitch) * n : 0;
+    a.in_misalign = 0;
+    for (const uint8_t* p : in) a.in_misalign |= static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u;
   }
 
   using namespace dev;
@@ -408,6 +424,20 @@ int main(int argc, char** argv) {
       case 16: KB_RINGS(16) break;
     }
   }
+  if (std::getenv("KB_REALIGN")) {  // aligned loads + in-register realignment (misaligned inputs)
+    static void (*const ra[8])(const ApplyArgs&, hipStream_t) = {
+#define KB_RA(R) [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, Policy<2, 1, true, true, false, 512, 2, 5, 0, false, true>>(a, s); }
+        KB_RA(1), KB_RA(2), KB_RA(3), KB_RA(4), KB_RA(5), KB_RA(6), KB_RA(7), KB_RA(8)};
+#undef KB_RA
+    static void (*const rc[8])(const ApplyArgs&, hipStream_t) = {
+#define KB_RA(R) [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, Policy<2, 1, true, true, false, 512, 2, 0, 0, false, true>>(a, s); }
+        KB_RA(1), KB_RA(2), KB_RA(3), KB_RA(4), KB_RA(5), KB_RA(6), KB_RA(7), KB_RA(8)};
+#undef KB_RA
+    if (m <= 8) {
+      vs.push_back(Variant{"realign g2", [m](const ApplyArgs& a, hipStream_t s) { ra[m - 1](a, s); }});
+      vs.push_back(Variant{"realign consec", [m](const ApplyArgs& a, hipStream_t s) { rc[m - 1](a, s); }});
+    }
+  }
   {  // memory ceiling of this traffic shape: the LDS kernel's loads/stores/grid, no lookups
     static void (*const nomath_g2[16])(const ApplyArgs&, hipStream_t) = {
 #define KB_NM(R) [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, Policy<2, 1, true, true, false, 512, (R > 8 ? 4 : 2), 5, (R > 8 ? 1 : 0), true>>(a, s); }
@@ -474,7 +504,7 @@ int main(int argc, char** argv) {
   CK(hipStreamSynchronize(s));
   CK(hipGetLastError());
   for (int b = 0; b < B; ++b)
-    CK(hipMemcpy(ref + static_cast<size_t>(b) * m * pitch, out[b * m], m * pitch, hipMemcpyDeviceToDevice));
+    CK(hipMemcpy(ref + static_cast<size_t>(b) * m * opitch, out[b * m], m * opitch, hipMemcpyDeviceToDevice));
 
   // KB_VERIFY=mask: rows with these bits compare against the parity just written
   // (upstream Verify) instead of storing; the status word must stay 0
@@ -482,7 +512,7 @@ int main(int argc, char** argv) {
   a.verify_mask = vmask;
   const double bytes = static_cast<double>(B) * S * n;
   std::vector<std::vector<double>> ms(vs.size());
-  std::vector<uint8_t> h1(m * pitch), h2(m * pitch);
+  std::vector<uint8_t> h1(m * opitch), h2(m * opitch);
   for (int rd = 0; rd < rounds; ++rd) {
     // rotate the order each round: the variant timed right after the D2D copy ran
     // ~3 % slow when it always went first
@@ -500,16 +530,16 @@ int main(int argc, char** argv) {
       ms[vi].push_back(t / iters);
       if (rd == 0 && vs[vi].check) {
         for (int b : {0, B / 2, B - 1}) {
-          CK(hipMemcpy(h1.data(), ref + static_cast<size_t>(b) * m * pitch, m * pitch, hipMemcpyDeviceToHost));
-          CK(hipMemcpy(h2.data(), out[b * m], m * pitch, hipMemcpyDeviceToHost));
+          CK(hipMemcpy(h1.data(), ref + static_cast<size_t>(b) * m * opitch, m * opitch, hipMemcpyDeviceToHost));
+          CK(hipMemcpy(h2.data(), out[b * m], m * opitch, hipMemcpyDeviceToHost));
           bool same = true;
-          for (int r = 0; r < m; ++r) same &= !std::memcmp(&h1[r * pitch], &h2[r * pitch], S);
+          for (int r = 0; r < m; ++r) same &= !std::memcmp(&h1[r * opitch], &h2[r * opitch], S);
           if (!same) std::printf("MISMATCH variant %s stripe %d\n", vs[vi].name.c_str(), b);
         }
       }
       if (!vs[vi].check && vs[vi].name.rfind("probe", 0) != 0) {  // restore parity clobbered by ceiling kernels
         for (int b = 0; b < B; ++b)
-          CK(hipMemcpy(out[b * m], ref + static_cast<size_t>(b) * m * pitch, m * pitch, hipMemcpyDeviceToDevice));
+          CK(hipMemcpy(out[b * m], ref + static_cast<size_t>(b) * m * opitch, m * opitch, hipMemcpyDeviceToDevice));
       }
     }
   }
