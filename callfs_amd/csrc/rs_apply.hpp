@@ -171,7 +171,7 @@ __global__ __launch_bounds__(P::BS) __attribute__((amdgpu_waves_per_eu(P::WPE, 8
 void rs_apply_vec(ApplyArgs a) {
   constexpr int U = P::U;
   constexpr int BS = P::BS;
-  const int K = KT ? KT : a.K;
+  const int K = a.K;
   const int npairs = K >> 1;
   const uint32_t tile_vecs = BS * U;
   const uint32_t tps = static_cast<uint32_t>((a.nvec + tile_vecs - 1) / tile_vecs);
