@@ -259,8 +259,10 @@ def main(argv=None):
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(el[0])
 
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    enc_all = sorted(e[0].elapsed_time(e[1]) for e in ev)
+    dec_all = sorted(e[1].elapsed_time(e[2]) for e in ev)
+    enc_ms = sum(enc_all) / args.steps
+    dec_ms = sum(dec_all) / args.steps
     user_step = 2 * B * k * (S_obj if S_obj else S * world)
     value = args.steps * user_step / elapsed / 2**30
 
@@ -299,6 +301,9 @@ def main(argv=None):
         "decode_gib_s": round(world * B * k * S / (dec_ms * 1e-3) / 2**30, 2),
         "encode_ms": round(enc_ms, 4),
         "decode_ms": round(dec_ms, 4),
+        # median and min per launch beside the mean the roofline uses
+        "encode_ms_median_min": [round(enc_all[len(enc_all) // 2], 4), round(enc_all[0], 4)],
+        "decode_ms_median_min": [round(dec_all[len(dec_all) // 2], 4), round(dec_all[0], 4)],
         "roofline": {
             "bound": "hbm",
             "kernel": ("rs_apply_lds" if k >= 4 else "rs_apply_vec") + " (encode plan)",

@@ -245,6 +245,11 @@ def test_concurrent_encodes_share_one_codec(codec):
 
 # ---- device-resident plans -----------------------------------------------------------
 
+def _mid(batch, seed):
+    """A seeded interior stripe index (checked beside the first and last)."""
+    return int(np.random.default_rng(seed).integers(0, batch)) if batch > 2 else 0
+
+
 def _batch(k, m, S, batch, seed):
     import torch
     from callfs_amd.device import StripeBatch
@@ -265,7 +270,7 @@ def test_plan_encode_matches_oracle(native_lib, k, m, S, batch):
     assert not plan.corrupt()
     torch.cuda.synchronize()
     host = sb.buf[:, :, :S].cpu().numpy()
-    for b in {0, batch - 1}:
+    for b in {0, _mid(batch, S), batch - 1}:
         want = cref.encode([host[b, i] for i in range(k)], k, m)
         for j in range(m):
             assert np.array_equal(host[b, k + j], want[j]), (b, j)
@@ -363,7 +368,7 @@ def test_plan_tile_orders_vs_oracle(native_lib, k, m, S, pitch, batch):
     torch.cuda.synchronize()
     view = buf.view(batch, n, pitch)[:, :, :S]
     want_all = view.cpu().numpy()
-    for b in {0, batch - 1}:
+    for b in {0, _mid(batch, S), batch - 1}:
         want = cref.encode([want_all[b, i] for i in range(k)], k, m)
         for j in range(m):
             assert np.array_equal(want_all[b, k + j], want[j]), (b, j)
@@ -783,7 +788,7 @@ def test_plan_launches_replay_in_a_hip_graph(native_lib):
         assert not dec.corrupt(s)
         host = sb.buf[:, :, :S].cpu().numpy()
         assert np.array_equal(host[:, :k], data.cpu().numpy())
-        for b in (0, batch - 1):
+        for b in sorted({0, _mid(batch, seed), batch - 1}):
             want = cref.encode([host[b, i] for i in range(k)], k, m)
             for j in range(m):
                 assert np.array_equal(host[b, k + j], want[j]), (seed, b, j)
@@ -841,7 +846,7 @@ def test_random_plans_vs_oracle(native_lib, k, m, S, batch, off, erase):
     torch.cuda.synchronize()
     host = buf.cpu().numpy()
     view = lambda b, i: host[off + (b * n + i) * pitch: off + (b * n + i) * pitch + S]
-    for b in {0, batch - 1}:
+    for b in {0, _mid(batch, S), batch - 1}:
         want = cref.encode([view(b, i).copy() for i in range(k)], k, m, simd=True, nthreads=4)
         for j in range(m):
             assert np.array_equal(view(b, k + j), want[j]), (b, j)
