@@ -451,6 +451,39 @@ __device__ __forceinline__ typename LdsAcc<RT>::T lds_zero() {
   else return 0;
 }
 
+// Byte r of a table entry / accumulator (row r's product for one data byte).
+template <int RT>
+__device__ __forceinline__ uint32_t lds_byte(const typename LdsAcc<RT>::T& t, int r) {
+  if constexpr (RT > 8) return (t.v[r >> 2] >> (8 * (r & 3))) & 0xffu;
+  else return static_cast<uint32_t>(t >> (8 * r)) & 0xffu;
+}
+
+// The ragged tail S % 16 of every shard, run by the stripe's last tile (one byte per
+// thread, the same LDS tables), so that launches with odd S need no second kernel
+// (launch_apply sets ApplyArgs::tail_in_vec). Entry e of input i's low / high table is
+// at lds0 + 32*W*i + W*e / + 16*W + W*e.
+template <int RT>
+__device__ __forceinline__ void lds_tail(const ApplyArgs& a, cptr<const uint8_t*> in,
+                                         cptr<uint8_t*> out, uint32_t stripe, uint32_t lds0) {
+  constexpr int W = LdsAcc<RT>::W;
+  const uint32_t nt = static_cast<uint32_t>(a.S - a.nvec * 16);
+  if (threadIdx.x >= nt) return;
+  const uint64_t b = a.nvec * 16 + threadIdx.x;
+  typename LdsAcc<RT>::T t = lds_zero<RT>();
+  for (int i = 0; i < a.K; ++i) {
+    const uint32_t x = in[i][b];
+    const uint32_t base = lds0 + static_cast<uint32_t>(i) * 32u * W;
+    t = t ^ lds_lookup<RT>(base + (x & 15u) * W) ^ lds_lookup<RT>(base + 16u * W + (x >> 4) * W);
+  }
+  bool bad = false;
+  for (int r = 0; r < a.R && r < RT; ++r) {
+    const uint8_t v = static_cast<uint8_t>(lds_byte<RT>(t, r));
+    if ((a.verify_mask >> r) & 1u) bad |= out[r][b] != v;
+    else out[r][b] = v;
+  }
+  if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
+}
+
 // Waves per SIMD the LDS kernel may be limited to: 16-byte entries keep 8 b128 reads
 // (32 VGPRs) in flight, which the register allocator only grants below 5 waves.
 template <int RT>
@@ -489,11 +522,12 @@ void rs_apply_lds(ApplyArgs a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t v0 = P::REALIGN ? static_cast<uint64_t>(tile) * TV + (threadIdx.x >> 6) * 63u + lane
                                    : static_cast<uint64_t>(tile) * BS + threadIdx.x;
+    cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
+    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
+    if (tile == tps - 1 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
     // lanes that store (REALIGN: lane 63 and lanes past the shard only load)
     const bool active = v0 < a.nvec && (!P::REALIGN || lane != 63u);
     if (P::REALIGN ? (v0 - lane >= a.nvec) : !active) continue;  // REALIGN: whole wave idle
-    cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
-    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
     auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
     AccT acc[4][4];
 #pragma unroll

@@ -178,11 +178,16 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
   uint64_t tail0 = 0;
+  a.tail_in_vec = 0;
   if (!bytes_only) {
     a.nvec = a.S / 16;
     tail0 = a.nvec * 16;
     if (a.nvec) {
       if (a.R >= kLdsMinRows || a.K >= kLdsMinK) {
+        // the LDS kernel's last tile per stripe computes the S % 16 tail itself: an odd-S
+        // launch (Split layout) is one kernel, not two back to back
+        a.tail_in_vec = tail0 < a.S;
+        if (a.tail_in_vec) tail0 = a.S;
         if (!a.ltabs) return hipErrorInvalidValue;
         const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];

@@ -489,6 +489,7 @@ typedef struct {
   size_t per;
   int next; /* atomic */
   int mismatches; /* atomic */
+  pthread_mutex_t* gate;
 } bench_t;
 
 static void bench_op(bench_t* B, int s, int op, size_t b0, size_t b1, uint8_t* tmp) {
@@ -546,6 +547,8 @@ typedef struct { bench_t* B; int tid; } bench_arg_t;
 
 static void* bench_thread(void* p) {
   bench_arg_t* a = (bench_arg_t*)p;
+  pthread_mutex_lock(a->B->gate); /* wait until the barriers are initialised */
+  pthread_mutex_unlock(a->B->gate);
   for (;;) {
     pthread_barrier_wait(&a->B->start);
     if (a->B->stop) return NULL;
@@ -634,21 +637,32 @@ int orc_bench_codec(int k, int m, size_t S, uint8_t* buf, size_t stripe_pitch,
   B->enc = make_sets(m, k, E + (size_t)k * k, &B->nenc);
   B->dec = make_sets(B->nmiss_d, k, drows, &B->ndec);
   B->par = make_sets(B->nmiss_p, k, prows, &B->npar);
+  const int ntmp = nthreads;
   B->tmp = (uint8_t**)calloc((size_t)nthreads, sizeof(uint8_t*));
   for (int t = 0; t < (mode == 0 ? nthreads : 1); t++) B->tmp[t] = (uint8_t*)malloc((size_t)m * S);
   /* byte ranges: 64-B aligned, at least 4 KiB, one per thread */
   B->per = (S + nthreads - 1) / nthreads;
   B->per = (B->per + 63) & ~(size_t)63;
   if (B->per < 4096) B->per = 4096;
-  pthread_barrier_init(&B->start, NULL, (unsigned)nthreads);
-  pthread_barrier_init(&B->end, NULL, (unsigned)nthreads);
+  /* the barriers count the threads that exist: if the system refuses a thread, run
+   * with the ones created so far instead of waiting forever at the first barrier */
   pthread_t th[POOL_MAX];
   bench_arg_t args[POOL_MAX];
+  pthread_mutex_t gate = PTHREAD_MUTEX_INITIALIZER;
+  pthread_mutex_lock(&gate); /* held until the barriers exist */
+  int made = 1;
+  B->gate = &gate;
   for (int t = 1; t < nthreads; t++) {
     args[t].B = B;
     args[t].tid = t;
-    pthread_create(&th[t], NULL, bench_thread, &args[t]);
+    if (pthread_create(&th[t], NULL, bench_thread, &args[t]) != 0) break;
+    made++;
   }
+  nthreads = made;
+  B->nthreads = made;
+  pthread_barrier_init(&B->start, NULL, (unsigned)nthreads);
+  pthread_barrier_init(&B->end, NULL, (unsigned)nthreads);
+  pthread_mutex_unlock(&gate);
   int passes = 0;
   const double t0 = mono_now();
   double el;
@@ -664,7 +678,7 @@ int orc_bench_codec(int k, int m, size_t S, uint8_t* buf, size_t stripe_pitch,
   if (elapsed_out) *elapsed_out = el;
   if (passes_out) *passes_out = passes;
   rc = B->mismatches;
-  for (int t = 0; t < nthreads; t++) free(B->tmp[t]);
+  for (int t = 0; t < ntmp; t++) free(B->tmp[t]);
   free(B->tmp);
   free(B->enc); free(B->dec); free(B->par);
 out:
