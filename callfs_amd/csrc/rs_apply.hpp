@@ -163,6 +163,34 @@ __device__ __forceinline__ void mac_one(uint32_t (&acc)[U][RT][4], const uint4 (
     }
 }
 
+// The ragged tail S % 16 of every shard, run by the stripe's last tile of the v_perm
+// kernel (one byte per thread): odd-S launches need no second kernel.
+template <int RT>
+__device__ __forceinline__ void vec_tail(const ApplyArgs& a, cptr<const uint8_t*> in,
+                                         cptr<uint8_t*> out, uint32_t stripe,
+                                         cptr<uint32_t> tabs) {
+  const uint32_t nt = static_cast<uint32_t>(a.S - a.nvec * 16);
+  if (threadIdx.x >= nt) return;
+  const uint64_t b = a.nvec * 16 + threadIdx.x;
+  uint32_t acc[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) acc[r] = 0;
+  for (int i = 0; i < a.K; ++i) {
+    const Sel sel = selectors(in[i][b]);
+    const cptr<uint32_t> t = tabs + static_cast<size_t>(i) * RT * 5;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r] = fma1(acc[r], gf_mul4(sel, t + r * 5));
+  }
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const uint8_t v = static_cast<uint8_t>(acc[r]);
+    if ((a.verify_mask >> r) & 1u) bad |= out[r][b] != v;
+    else out[r][b] = v;
+  }
+  if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
+}
+
 // Tiles: a stripe's nvec vectors are cut into tiles of BS*U; tile t covers stripe
 // t / tiles_per_stripe (ORD 0) or t % batch (ORD 1). Every tile is wave-uniform in its
 // stripe, so shard pointers stay scalar.
@@ -189,6 +217,7 @@ void rs_apply_vec(ApplyArgs a) {
     const uint64_t v0 = static_cast<uint64_t>(tile) * tile_vecs + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * RT;
+    if (tile == tps - 1 && a.tail_in_vec) vec_tail<RT>(a, in, out, stripe, tabs);
     bool live[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) live[u] = v0 + static_cast<uint64_t>(u) * BS < a.nvec;

@@ -229,6 +229,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
           hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, a);
         });
       } else {
+        a.tail_in_vec = tail0 < a.S;  // as for the LDS kernel: the last tile takes the tail
+        if (a.tail_in_vec) tail0 = a.S;
         VecFn fn = kVec[a.R - 1];  // R <= 4 here (R >= kLdsMinRows takes the LDS kernel)
         const uint64_t tps = (a.nvec + ProdPolicy::BS - 1) / ProdPolicy::BS;
         switch (vec_tile_order(a.S, tps, a.addr_tz)) {
