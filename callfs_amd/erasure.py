@@ -155,7 +155,10 @@ class Codec:
         """codec.go:21-41. Returns data_shards+parity_shards equal-length shards: S =
         ceil(len/k); like upstream Split the full data shards are views into `data`
         (no copy), the shard holding the end of the object and any after it are
-        zero-padded copies, and only the m parity shards are computed (rs_encode)."""
+        zero-padded copies, and only the m parity shards are computed (rs_encode).
+        Upstream Split also reuses a Go slice's spare capacity past len for the padded
+        and parity shards; Python buffers expose no such capacity, so this mirror always
+        allocates them (the Go shim, go/erasure/codec_rocm.go split, does reuse it)."""
         k, m = profile.data_shards, profile.parity_shards
         if k < 1 or m < 1:
             raise ErrInvalidProfile()
