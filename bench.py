@@ -66,6 +66,9 @@ def parse_args(argv=None):
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="CPU baseline threads (0: the visible cores, at most 16 -- the "
                         "GPU box's CPU share per GPU)")
+    p.add_argument("--tune", type=int, default=1,
+                   help="1: rs_plan_tune each plan before the warmup (times every tile order "
+                        "its kernel offers on this box and keeps the fastest; 0: the rule)")
     p.add_argument("--copy-ceiling", type=int, default=1,
                    help="1: also time a device copy of the same bytes (roofline.copy_ceiling)")
     p.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
@@ -227,6 +230,11 @@ def main(argv=None):
         raise SystemExit("device round trip failed")
     del ref
 
+    # untimed: pick each plan's tile order on this box (the outputs are recomputed to the
+    # same bytes; DESIGN.md §5 "Tile order")
+    orders = ({"encode": enc.tune(stream=stream), "decode": dec.tune(stream=stream)}
+              if args.tune else None)
+
     for _ in range(args.warmup):
         enc.launch(stream)
         dec.launch(stream)
@@ -294,6 +302,8 @@ def main(argv=None):
             # decode re-verifies only the present parity beyond the first k (a9): none
             # when exactly k shards survive, as with the default 4-of-14 erasure
             "decode_verify_rows": verify_rows,
+            # per launch group, chosen by rs_plan_tune before the warmup (None: the rule)
+            "tile_order": orders,
             "parallelism": (f"byte-column slices over {world} GPU(s), no collective" if S_obj
                             else f"stripes sharded over {world} GPU(s), no collective"),
         },

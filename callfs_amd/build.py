@@ -6,6 +6,7 @@ next to this file so it travels to the GPU box with the repo snapshot.
 from __future__ import annotations
 
 import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -13,6 +14,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcallfs_rs.so")
+# Per-kernel register / scratch / occupancy report of the last build (the compiler's
+# kernel-resource-usage remarks), checked by tests/test_kernel_resources.py: the LDS
+# kernel's speed depends on its waves per SIMD.
+RESOURCES = os.path.join(HERE, "kernel_resources.json")
 SOURCES = ["rs_kernels.hip", "sha256.hip", "rs_capi.cpp"]
 HEADERS = ["rs_kernels.hpp", "rs_apply.hpp", "tile_order.hpp", "gf256.hpp", "copy_pool.hpp", "dispatch.hpp", "sha256.hpp", os.path.join("..", "..", "include", "callfs_rs.h")]
 ARCH = os.environ.get("CALLFS_OFFLOAD_ARCH", "gfx950")
@@ -48,13 +53,22 @@ def build(force: bool = False, extra_flags=None) -> str:
     objs = []
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
              "-Wno-unused-result", "-Wno-cuda-compat"] + list(extra_flags or [])
+    kernels = []
     for src in SOURCES:
         obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
         cmd = [_hipcc(), *flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if src.endswith(".cpp"):
             cmd.insert(1, "-x")
             cmd.insert(2, "hip")
-        subprocess.run(cmd, check=True)
+        else:
+            cmd.append("-Rpass-analysis=kernel-resource-usage")
+        r = subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
+        kernels += _parse_resource_remarks(r.stderr)
+        other = [ln for ln in r.stderr.splitlines() if "kernel-resource-usage" not in ln]
+        if r.returncode != 0 or any("error" in ln or "warning" in ln for ln in other):
+            sys.stderr.write("\n".join(other) + "\n")
+        if r.returncode != 0:
+            raise subprocess.CalledProcessError(r.returncode, cmd)
         objs.append(obj)
     tmp = LIB + ".tmp"
     subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp],
@@ -62,9 +76,51 @@ def build(force: bool = False, extra_flags=None) -> str:
     os.replace(tmp, LIB)
     for o in objs:
         os.remove(o)
+    with open(RESOURCES, "w") as fh:
+        json.dump({"digest": _digest(), "arch": ARCH, "kernels": kernels}, fh, indent=1)
+        fh.write("\n")
     with open(LIB + ".sha256", "w") as fh:
         fh.write(_digest())
     return LIB
+
+
+def _parse_resource_remarks(text: str) -> list:
+    """Kernel name, VGPRs, scratch bytes per lane, spills and occupancy from the
+    `-Rpass-analysis=kernel-resource-usage` remarks hipcc prints per kernel."""
+    out, cur = [], None
+    keys = {"VGPRs": "vgprs", "AGPRs": "agprs", "ScratchSize [bytes/lane]": "scratch",
+            "Occupancy [waves/SIMD]": "waves_per_simd", "VGPRs Spill": "vgpr_spill",
+            "SGPRs Spill": "sgpr_spill", "TotalSGPRs": "sgprs"}
+    for ln in text.splitlines():
+        if "remark:" not in ln or "kernel-resource-usage" not in ln:
+            continue
+        body = ln.split("remark:", 1)[1].rsplit("[-Rpass", 1)[0].strip()
+        if body.startswith("Function Name:"):
+            cur = {"symbol": body.split(":", 1)[1].strip()}
+            out.append(cur)
+        elif cur is not None and ":" in body:
+            k, v = body.rsplit(":", 1)
+            if k.strip() in keys:
+                try:
+                    cur[keys[k.strip()]] = int(v.strip())
+                except ValueError:
+                    pass
+    names = _demangle([k["symbol"] for k in out])
+    for k, n in zip(out, names):
+        k["name"] = n
+    return out
+
+
+def _demangle(symbols: list) -> list:
+    try:
+        r = subprocess.run(["c++filt"], input="\n".join(symbols), capture_output=True,
+                           text=True, check=True)
+        names = r.stdout.splitlines()
+        if len(names) == len(symbols):
+            return names
+    except (OSError, subprocess.CalledProcessError):
+        pass
+    return list(symbols)
 
 
 if __name__ == "__main__":

@@ -96,9 +96,12 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //            vector by DPP wave_shl:1, v_alignbyte funnel shift) instead of unaligned
 //            global_load_dwordx4
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
-          int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, bool REALIGN_ = false>
+          int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, bool REALIGN_ = false,
+          bool SDWA_ = false>
 struct Policy {
   static constexpr bool NOMATH = NOMATH_;
+  // LDS table addresses by v_or_b32_sdwa (byte select + OR) instead of v_perm_b32
+  static constexpr bool SDWA = SDWA_;
   static constexpr bool REALIGN = REALIGN_;
   // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads
   static constexpr int TILE_VECS = REALIGN_ ? BS_ / 64 * 63 : BS_ * U_;
@@ -406,11 +409,30 @@ __device__ __forceinline__ u32x4_acc lds_x3(const u32x4_acc& a, const u32x4_acc&
                     xor3(a.v[2], b.v[2], c.v[2]), xor3(a.v[3], b.v[3], c.v[3])}};
 }
 
+// base | byte J of x in one v_or_b32_sdwa (SDWA source select; base in an SGPR).
+template <int J>
+__device__ __forceinline__ uint32_t or_byte(uint32_t x, uint32_t base) {
+  uint32_t r;
+  if constexpr (J == 0)
+    asm("v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+        : "=v"(r) : "v"(x), "s"(base));
+  else if constexpr (J == 1)
+    asm("v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+        : "=v"(r) : "v"(x), "s"(base));
+  else if constexpr (J == 2)
+    asm("v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+        : "=v"(r) : "v"(x), "s"(base));
+  else
+    asm("v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+        : "=v"(r) : "v"(x), "s"(base));
+  return r;
+}
+
 // base: absolute LDS address of input shard i's tables (256-B aligned).
 // All 8 lookups of a data dword are issued before any is consumed; for 16-byte entries
 // a sched_group_barrier keeps them together (the default schedule reused one register
 // quad and waited after every pair: 2 reads in flight instead of 8).
-template <int RT>
+template <int RT, bool SD = false>
 __device__ __forceinline__ void lds_mac(typename LdsAcc<RT>::T (&acc)[4][4], const uint4& x,
                                         uint32_t base) {
   using T = typename LdsAcc<RT>::T;
@@ -429,11 +451,24 @@ __device__ __forceinline__ void lds_mac(typename LdsAcc<RT>::T (&acc)[4][4], con
       base_hi = base + 256u;
     }
     T lo[4], hi[4];
+    if constexpr (SD) {
+      const uint32_t sb = __builtin_amdgcn_readfirstlane(base);
+      const uint32_t sbh = __builtin_amdgcn_readfirstlane(base_hi);
+      lo[0] = lds_lookup<RT>(or_byte<0>(xl, sb));
+      hi[0] = lds_lookup<RT>(or_byte<0>(xh, sbh));
+      lo[1] = lds_lookup<RT>(or_byte<1>(xl, sb));
+      hi[1] = lds_lookup<RT>(or_byte<1>(xh, sbh));
+      lo[2] = lds_lookup<RT>(or_byte<2>(xl, sb));
+      hi[2] = lds_lookup<RT>(or_byte<2>(xh, sbh));
+      lo[3] = lds_lookup<RT>(or_byte<3>(xl, sb));
+      hi[3] = lds_lookup<RT>(or_byte<3>(xh, sbh));
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t sel = 0x07060500u | static_cast<uint32_t>(j);
-      lo[j] = lds_lookup<RT>(__builtin_amdgcn_perm(base, xl, sel));
-      hi[j] = lds_lookup<RT>(__builtin_amdgcn_perm(base_hi, xh, sel));
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t sel = 0x07060500u | static_cast<uint32_t>(j);
+        lo[j] = lds_lookup<RT>(__builtin_amdgcn_perm(base, xl, sel));
+        hi[j] = lds_lookup<RT>(__builtin_amdgcn_perm(base_hi, xh, sel));
+      }
     }
     if constexpr (W == 16) {
       __builtin_amdgcn_sched_group_barrier(0x0100, 8, 0);  // the 8 DS reads
@@ -483,7 +518,11 @@ __device__ __forceinline__ typename LdsAcc<RT>::T lds_zero() {
 // Byte r of a table entry / accumulator (row r's product for one data byte).
 template <int RT>
 __device__ __forceinline__ uint32_t lds_byte(const typename LdsAcc<RT>::T& t, int r) {
-  if constexpr (RT > 8) return (t.v[r >> 2] >> (8 * (r & 3))) & 0xffu;
+  if constexpr (RT > 8) {  // select, not an indexed load: a runtime index into t.v would
+                          // put the accumulator in scratch for the whole kernel
+    const uint32_t q = r < 4 ? t.v[0] : r < 8 ? t.v[1] : r < 12 ? t.v[2] : t.v[3];
+    return (q >> (8 * (r & 3))) & 0xffu;
+  }
   else return static_cast<uint32_t>(t >> (8 * r)) & 0xffu;
 }
 
@@ -572,7 +611,7 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll 1
       for (int i = 0; i < K; ++i) {
         if (i + 2 < K) x2 = lda(i + 2);
-        lds_mac<RT>(acc, realign(in[i], x0), lds0 + static_cast<uint32_t>(i) * 32u * W);
+        lds_mac<RT, P::SDWA>(acc, realign(in[i], x0), lds0 + static_cast<uint32_t>(i) * 32u * W);
         x0 = x1;
         x1 = x2;
       }
@@ -586,7 +625,7 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll
           for (int w = 0; w < 4; ++w) acc[w][0] = acc[w][0] ^ lds_splat<RT>(word(x0, w));
         } else {
-          lds_mac<RT>(acc, x0, lds0 + static_cast<uint32_t>(i) * 32u * W);
+          lds_mac<RT, P::SDWA>(acc, x0, lds0 + static_cast<uint32_t>(i) * 32u * W);
         }
         x0 = x1;
         x1 = x2;
@@ -608,7 +647,7 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll
               for (int w = 0; w < 4; ++w) acc[w][0] = acc[w][0] ^ lds_splat<RT>(word(xr[s], w));
             } else {
-              lds_mac<RT>(acc, xr[s], lds0 + static_cast<uint32_t>(i) * 32u * W);
+              lds_mac<RT, P::SDWA>(acc, xr[s], lds0 + static_cast<uint32_t>(i) * 32u * W);
             }
           }
         }

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
@@ -324,26 +325,35 @@ LayoutHint fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h
   return hint;
 }
 
+ApplyArgs group_args(const Tables& t, const MetaLayout& L, size_t gi, int batch, uint8_t* d,
+                     size_t S, int status_stride, const LayoutHint& hint) {
+  const Group& g = t.groups[gi];
+  ApplyArgs a{};
+  a.in_tab = reinterpret_cast<const uint8_t* const*>(d + L.in_off);
+  a.out_tab = reinterpret_cast<uint8_t* const*>(d + L.out_off[gi]);
+  a.tabs = reinterpret_cast<const uint32_t*>(d + L.tab_off[gi]);
+  a.ltabs = d + L.ltab_off[gi];
+  a.S = S;
+  a.verify_mask = g.verify_mask;
+  a.status = reinterpret_cast<int*>(d + L.status_off);
+  a.status_stride = status_stride;
+  a.K = t.k;
+  a.R = static_cast<int>(g.shard.size());
+  a.batch = batch;
+  a.addr_tz = hint.addr_tz;
+  a.stripe_stride = hint.stripe_stride;
+  a.in_misalign = hint.in_misalign;
+  return a;
+}
+
+// orders: per launch group, a TileOrder from rs_plan_tune or -1 (the rule); null = rule.
 hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_t* d, size_t S,
-                         hipStream_t s, int status_stride, const LayoutHint& hint) {
+                         hipStream_t s, int status_stride, const LayoutHint& hint,
+                         const std::vector<int>* orders = nullptr) {
   for (size_t gi = 0; gi < t.groups.size(); ++gi) {
-    const Group& g = t.groups[gi];
-    ApplyArgs a{};
-    a.in_tab = reinterpret_cast<const uint8_t* const*>(d + L.in_off);
-    a.out_tab = reinterpret_cast<uint8_t* const*>(d + L.out_off[gi]);
-    a.tabs = reinterpret_cast<const uint32_t*>(d + L.tab_off[gi]);
-    a.ltabs = d + L.ltab_off[gi];
-    a.S = S;
-    a.verify_mask = g.verify_mask;
-    a.status = reinterpret_cast<int*>(d + L.status_off);
-    a.status_stride = status_stride;
-    a.K = t.k;
-    a.R = static_cast<int>(g.shard.size());
-    a.batch = batch;
-    a.addr_tz = hint.addr_tz;
-    a.stripe_stride = hint.stripe_stride;
-    a.in_misalign = hint.in_misalign;
-    hipError_t e = launch_apply(a, s);
+    const int order = orders && gi < orders->size() ? (*orders)[gi] : -1;
+    hipError_t e = launch_apply(group_args(t, L, gi, batch, d, S, status_stride, hint), s,
+                                /*bytes_only=*/false, order);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -1288,6 +1298,8 @@ struct rs_plan {
   void* dmeta = nullptr;
   uint64_t bytes = 0;
   LayoutHint hint;
+  std::vector<int> orders;  // per launch group: tile order from rs_plan_tune, -1 = rule
+  std::mutex mu;            // orders are written by rs_plan_tune, read by rs_plan_launch
 };
 
 int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
@@ -1334,9 +1346,102 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
   DeviceGuard dg;
   if (!plan) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
+  std::vector<int> orders;
+  {
+    std::lock_guard<std::mutex> g(plan->mu);
+    orders = plan->orders;
+  }
   HIPCHK(launch_groups(*plan->tables, plan->layout, plan->batch,
                        static_cast<uint8_t*>(plan->dmeta), plan->S,
-                       static_cast<hipStream_t>(stream), /*status_stride=*/1, plan->hint));
+                       static_cast<hipStream_t>(stream), /*status_stride=*/1, plan->hint,
+                       &orders));
+  return RS_OK;
+}
+
+// Times every tile order each launch group's kernel offers and keeps the fastest. Which
+// order HBM serves best varies between MI355X boxes by 1-2 points on the same shape
+// (DESIGN.md §5 "Tile order"), so a plan that is launched many times measures it on the
+// box it runs on, like a library autotuner, instead of trusting the rule alone. Each
+// candidate gets `reps` back-to-back launches between two events, in three rounds with the
+// candidate order rotated; the per-launch mean of the best round counts, and the rule's
+// order is kept unless another is faster by more than 0.3 %.
+namespace {
+constexpr int kTuneRounds = 3;
+// CALLFS_RS_TUNE_LOG=1: rs_plan_tune prints each candidate's time per launch to stderr
+bool tune_log() {
+  static const bool on = [] {
+    const char* e = std::getenv("CALLFS_RS_TUNE_LOG");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
+}  // namespace
+
+int rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups) {
+  DeviceGuard dg;
+  if (!plan || reps < 1 || max_groups < 0 || (max_groups > 0 && !orders)) return RS_E_ARG;
+  HIPCHK(hipSetDevice(plan->device));
+  auto s = static_cast<hipStream_t>(stream);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIPCHK(hipStreamIsCapturing(s, &cap));
+  if (cap != hipStreamCaptureStatusNone) return RS_E_ARG;  // synchronous: not in a capture
+  const Tables& t = *plan->tables;
+  auto* d = static_cast<uint8_t*>(plan->dmeta);
+  std::vector<int> chosen(t.groups.size(), -1);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIPCHK(hipEventCreate(&e0));
+  if (hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return RS_E_HIP;
+  }
+  int rc = RS_OK;
+  for (size_t gi = 0; gi < t.groups.size() && rc == RS_OK; ++gi) {
+    const ApplyArgs a = group_args(t, plan->layout, gi, plan->batch, d, plan->S, 1, plan->hint);
+    const std::vector<int> cand = order_candidates(a);
+    if (cand.size() < 2) continue;
+    std::vector<float> best(cand.size(), 1e30f);
+    // warm-up in the rule's order first: the first candidate timed right after other
+    // work (the bench's round-trip check) measured up to 3 % slow
+    for (int r = 0; r < reps && rc == RS_OK; ++r)
+      if (launch_apply(a, s, false, cand[0]) != hipSuccess) rc = RS_E_HIP;
+    for (int round = 0; round < kTuneRounds && rc == RS_OK; ++round) {
+      for (size_t j = 0; j < cand.size() && rc == RS_OK; ++j) {
+        const size_t c = (j + round) % cand.size();
+        // one untimed launch, then `reps` timed ones
+        bool ok = launch_apply(a, s, false, cand[c]) == hipSuccess && hipEventRecord(e0, s) == hipSuccess;
+        for (int r = 0; r < reps && ok; ++r) ok = launch_apply(a, s, false, cand[c]) == hipSuccess;
+        ok = ok && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess;
+        float ms = 0;
+        ok = ok && hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+        if (!ok) {
+          rc = RS_E_HIP;
+          break;
+        }
+        best[c] = std::min(best[c], ms / static_cast<float>(reps));
+      }
+    }
+    if (rc != RS_OK) break;
+    size_t win = 0;  // cand[0] is the rule's order
+    for (size_t c = 1; c < cand.size(); ++c)
+      if (best[c] < best[win] * (win == 0 ? 0.997f : 1.0f)) win = c;
+    chosen[gi] = cand[win];
+    if (tune_log()) {
+      std::fprintf(stderr, "rs_plan_tune: group %zu (K=%d R=%d S=%zu batch=%d):", gi, a.K, a.R,
+                   static_cast<size_t>(a.S), a.batch);
+      for (size_t c = 0; c < cand.size(); ++c)
+        std::fprintf(stderr, " order %d %.1f us%s", cand[c], best[c] * 1e3f, c == win ? " *" : "");
+      std::fprintf(stderr, "\n");
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc != RS_OK) return rc;
+  {
+    std::lock_guard<std::mutex> g(plan->mu);
+    plan->orders = chosen;
+  }
+  for (int i = 0; i < max_groups; ++i)
+    orders[i] = static_cast<size_t>(i) < chosen.size() ? chosen[i] : -1;
   return RS_OK;
 }
 

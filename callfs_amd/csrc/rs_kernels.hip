@@ -41,8 +41,15 @@ using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
 // 5-slot ring. RS(10,12) 61.5 -> 68.0 %, RS(10,16) 63.2 -> 69.3 %, RS(20,16) 59.3 ->
 // 60.7 % of 8 TB/s (tools/kbench.hip, KB_RING). For R <= 8 the unrolled ring measured
 // 1-3 % slower than the shifted ring of three, so those keep LdsPolicy.
-using LdsWidePolicy = dev::Policy<2, 1, true, true, false, 512, 4, 0, 1>;
-using LdsWideQ8Policy = dev::Policy<2, 1, true, true, false, 512, 4, 6, 1>;
+// Their table addresses are formed by v_or_b32_sdwa (byte select + OR with an SGPR
+// base) instead of v_perm_b32: same issue rate (tools/valu_rates.hip, 0.24 per SIMD
+// clock), but no VGPR for the table base, which keeps R = 16 at 125 VGPRs (4 waves per
+// SIMD; the v_perm form had grown to 129 = 3 waves once the ragged tail moved into the
+// kernel). tools/sdwa_sweep.sh, profiles/r02/sdwa/, % of 8 TB/s, v_perm -> SDWA:
+// RS(10,16) 58.3 -> 66.8, RS(20,16) 52.2 -> 59.3, RS(32,16) 49.0 -> 55.0, RS(10,12)
+// 65.9 -> 66.5.
+using LdsWidePolicy = dev::Policy<2, 1, true, true, false, 512, 4, 0, 1, false, false, true>;
+using LdsWideQ8Policy = dev::Policy<2, 1, true, true, false, 512, 4, 6, 1, false, false, true>;
 template <int R>
 using LdsPolicyFor = typename std::conditional<(R > 8), LdsWidePolicy, LdsPolicy>::type;
 using LdsG8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 2>;
@@ -173,7 +180,66 @@ void set_slice_tiles_for_tuning(long long tiles) {
   g_slice_tiles_override.store(tiles, std::memory_order_relaxed);
 }
 
-hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
+namespace {
+
+TileOrder lds_rule(const ApplyArgs& a) {
+  const int forced = tile_order_override();
+  if (forced >= 0) return static_cast<TileOrder>(forced);
+  return lds_tile_order(a.S, (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS, a.addr_tz, a.K + a.R,
+                        a.stripe_stride);
+}
+
+TileOrder wide_rule(const ApplyArgs& a) {
+  return wide_tile_order((a.nvec + LdsWidePolicy::BS - 1) / LdsWidePolicy::BS);
+}
+
+TileOrder vec_rule(const ApplyArgs& a) {
+  return vec_tile_order(a.S, (a.nvec + ProdPolicy::BS - 1) / ProdPolicy::BS, a.addr_tz);
+}
+
+bool takes_lds(const ApplyArgs& a) { return a.R >= kLdsMinRows || a.K >= kLdsMinK; }
+bool takes_realign(const ApplyArgs& a) {
+  return a.R <= 8 && a.in_misalign && a.K >= kRealignMinK;
+}
+
+}  // namespace
+
+std::vector<int> order_candidates(const ApplyArgs& a0) {
+  ApplyArgs a = a0;
+  a.nvec = a.S / 16;
+  std::vector<int> c;
+  auto add = [&c](TileOrder o) {
+    const int v = static_cast<int>(o);
+    if (std::find(c.begin(), c.end(), v) == c.end()) c.push_back(v);
+  };
+  if (a.nvec == 0 || a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1) return c;
+  const uint64_t tps = (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;
+  if (takes_lds(a)) {
+    if (a.R > 8) {
+      add(wide_rule(a));
+      add(TileOrder::kConsecutive);
+      add(TileOrder::kSeg8);
+      return c;
+    }
+    if (takes_realign(a)) return c;
+    add(lds_rule(a));
+    add(TileOrder::kConsecutive);
+    add(TileOrder::kGroup2);
+    if (tps <= 32) add(TileOrder::kGroup8);
+    if (tps > 1024) {
+      add(TileOrder::kSeg8);
+      add(TileOrder::kSeg16);
+    }
+    return c;
+  }
+  add(vec_rule(a));
+  add(TileOrder::kConsecutive);
+  add(TileOrder::kGroup2);
+  if (tps > 1024) add(TileOrder::kSeg16);
+  return c;
+}
+
+hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int order) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
@@ -183,7 +249,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
     a.nvec = a.S / 16;
     tail0 = a.nvec * 16;
     if (a.nvec) {
-      if (a.R >= kLdsMinRows || a.K >= kLdsMinK) {
+      if (takes_lds(a)) {
         // the LDS kernel's last tile per stripe computes the S % 16 tail itself: an odd-S
         // launch (Split layout) is one kernel, not two back to back
         a.tail_in_vec = tail0 < a.S;
@@ -192,18 +258,14 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
-          const int forced = tile_order_override();
-          switch (forced >= 0 ? static_cast<TileOrder>(forced)
-                              : lds_tile_order(a.S, (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS,
-                                               a.addr_tz, a.K + a.R, a.stripe_stride)) {
+          switch (order >= 0 ? static_cast<TileOrder>(order) : lds_rule(a)) {
             case TileOrder::kGroup8: fn = kLdsG8[a.R - 1]; break;
             case TileOrder::kGroup2: fn = kLdsG2[a.R - 1]; break;
             case TileOrder::kSeg8: fn = kLdsQ8[a.R - 1]; break;
             case TileOrder::kSeg16: fn = kLdsQ16[a.R - 1]; break;
             case TileOrder::kConsecutive: break;
           }
-        } else if (wide_tile_order((a.nvec + LdsWidePolicy::BS - 1) / LdsWidePolicy::BS) ==
-                   TileOrder::kSeg8) {
+        } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }
         if (lds > (64u << 10)) {  // wide groups with many shards: opt in once per kernel
@@ -221,7 +283,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
                           LdsWideQ8Policy::BS == LdsPolicy::BS && LdsRealignPolicy::BS == LdsPolicy::BS,
                       "one grid shape for every LDS policy");
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
-        if (a.R <= 8 && a.in_misalign && a.K >= kRealignMinK) {
+        if (takes_realign(a)) {
           fn = kLdsRealign[a.R - 1];
           gx = dev::vec_grid<LdsRealignPolicy>(a.nvec, a.batch);
         }
@@ -232,8 +294,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only) {
         a.tail_in_vec = tail0 < a.S;  // as for the LDS kernel: the last tile takes the tail
         if (a.tail_in_vec) tail0 = a.S;
         VecFn fn = kVec[a.R - 1];  // R <= 4 here (R >= kLdsMinRows takes the LDS kernel)
-        const uint64_t tps = (a.nvec + ProdPolicy::BS - 1) / ProdPolicy::BS;
-        switch (vec_tile_order(a.S, tps, a.addr_tz)) {
+        switch (order >= 0 ? static_cast<TileOrder>(order) : vec_rule(a)) {
           case TileOrder::kGroup2: fn = kVecG2[a.R - 1]; break;
           case TileOrder::kSeg16: fn = kVecQ16[a.R - 1]; break;
           default: break;

@@ -2,6 +2,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <vector>
 #include <cstdint>
 
 namespace callfs {
@@ -60,7 +62,15 @@ inline int shard_addr_tz(const void* const* p, int count) {
 // offsets (upstream Split layout of a contiguous object) that ran 4.7x the byte kernel
 // (DESIGN.md §5). bytes_only forces the byte kernel over all of [0, S) (kbench A/B).
 // Returns hipSuccess or the launch error.
-hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false);
+// `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
+// chosen kernel has an instance in that order (order_candidates lists them); -1 = the
+// rule (or CALLFS_RS_TILE_ORDER).
+hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false, int order = -1);
+
+// Tile orders worth timing for launch `a` (rs_plan_tune): the rule's choice first, then
+// the alternatives that have kernel instances for this path. Empty when the launch has
+// no choice (byte kernel, realigning kernel, S < 16).
+std::vector<int> order_candidates(const ApplyArgs& a);
 
 // Tuning hook for tools/kbench.hip (not part of the C ABI): tiles per launch slice for
 // every later launch_apply in the process; 0 = never slice, < 0 = the built-in rule

@@ -95,6 +95,19 @@ class Plan:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         N.check(N.lib.rs_plan_launch(self.handle, ctypes.c_void_p(s.cuda_stream)), "rs_plan_launch")
 
+    ORDER_NAMES = {-1: "none", 0: "consecutive", 1: "g8", 2: "g2", 3: "q8", 4: "q16"}
+
+    def tune(self, reps: int = 5, stream: Optional[torch.cuda.Stream] = None) -> list:
+        """rs_plan_tune: time each launch group in every tile order its kernel offers
+        and keep the fastest for later launches (synchronous; outputs recomputed to the
+        same bytes). Returns the chosen order name per launch group."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        n = max(1, -(-self.m // 16))  # launch groups: at most ceil(m / 16) rows of 16
+        orders = (ctypes.c_int * n)()
+        N.check(N.lib.rs_plan_tune(self.handle, ctypes.c_void_p(s.cuda_stream), reps, orders, n),
+                "rs_plan_tune")
+        return [self.ORDER_NAMES.get(orders[i], str(orders[i])) for i in range(n)]
+
     def corrupt(self, stream: Optional[torch.cuda.Stream] = None) -> bool:
         """Synchronises the stream; True when a Verify row mismatched (then clears)."""
         s = stream if stream is not None else torch.cuda.current_stream(self.device)

@@ -161,6 +161,23 @@ int  rs_plan_stripe_status(rs_plan* plan, void* stream, int* flags);
 uint64_t rs_plan_bytes(const rs_plan* plan);
 void rs_plan_destroy(rs_plan* plan);
 
+/* Tile-order tuning (no upstream counterpart; an autotuner for repeated launches).
+ * Which order of column tiles HBM serves best for a shape varies between MI355X boxes
+ * by 1-2 %. rs_plan_tune times each launch group of the plan in every
+ * tile order its kernel offers (`reps` launches per order, three rounds) and keeps the
+ * fastest for later rs_plan_launch calls; the measured rule's order stays unless another
+ * is > 0.3 % faster. Synchronous on `stream`; RS_E_ARG while `stream` is capturing. The
+ * tuning launches recompute the plan's outputs from its inputs (same bytes; Verify rows
+ * may flag status exactly as rs_plan_launch would). orders (NULL when max_groups == 0):
+ * the chosen order per launch group, up to max_groups entries (RS_ORDER_* or -1 = the
+ * launch has no choice). */
+#define RS_ORDER_CONSECUTIVE 0
+#define RS_ORDER_GROUP8 1
+#define RS_ORDER_GROUP2 2
+#define RS_ORDER_SEG8 3
+#define RS_ORDER_SEG16 4
+int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups);
+
 /* One-shot device-resident calls (build + launch + free; tables cached per profile).
  * Same pointer layout as rs_plan_create; synchronous on `stream`. rs_decode_dev
  * returns RS_E_CORRUPT when the verify rows mismatch. */

@@ -1080,3 +1080,65 @@ def test_plan_misaligned_batch_realign(native_lib, k, m, S, batch, off):
         dec.launch()
         assert not dec.corrupt(), erase
         assert np.array_equal(buf.cpu().numpy()[off:off + total], host), erase
+
+
+# ---- tile-order tuning (rs_plan_tune) ----------------------------------------------------
+
+@pytest.mark.parametrize("k,m,S,batch,erase", [
+    (10, 4, 1 << 20, 6, None),          # LDS kernel, rule G2: consecutive / G2 timed
+    (10, 4, 1 << 20, 6, (0, 3, 7)),     # decode with a Verify row
+    (3, 2, 349_526, 8, None),           # v_perm kernel
+    (10, 16, 262_144 + 5, 3, None),     # wide group (SDWA addresses), ragged tail
+    (20, 20, 65_536, 4, None),          # two launch groups (16 + 4 rows)
+    (4, 2, 96, 40, None),               # one tile per stripe: G8 among the candidates
+])
+def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
+    """rs_plan_tune launches every candidate order (the outputs are recomputed to the same
+    bytes) and later launches use the chosen one: parity / reconstruction stay bit-exact
+    against the oracle, and Verify does not flag clean stripes."""
+    import torch
+    from callfs_amd.device import Plan
+    sb = _batch(k, m, S, batch, seed=S + k)
+    enc = Plan.for_batch(sb)
+    names = enc.tune(reps=1)
+    assert len(names) == max(1, -(-m // 16))
+    assert all(n in {"consecutive", "g8", "g2", "q8", "q16"} for n in names), names
+    sb.fill_random(S + k + 1)  # fresh data: the tuned plan must compute it, not reuse
+    enc.launch()
+    torch.cuda.synchronize()
+    host = sb.buf[:, :, :S].cpu().numpy()
+    for b in sorted({0, _mid(batch, S), batch - 1}):
+        want = cref.encode([host[b, i] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(host[b, k + j], want[j]), (b, j)
+    if erase is None:
+        return
+    ref = sb.buf.clone()
+    present = [i not in erase for i in range(k + m)]
+    dec = Plan.for_batch(sb, present=present)
+    for i in erase:
+        sb.buf[:, i].zero_()
+    dec.tune(reps=2)
+    assert not dec.corrupt()
+    for i in erase:
+        sb.buf[:, i].zero_()
+    dec.launch()
+    assert not dec.corrupt()
+    assert torch.equal(sb.buf[:, :, :S], ref[:, :, :S])
+    sb.buf[1, 13, 77] ^= 4  # parity 13 is a Verify row of this pattern
+    dec.launch()
+    assert dec.corrupt_stripes() == [1]
+
+
+def test_plan_tune_argument_errors(native_lib):
+    import ctypes
+    from callfs_amd import _native as N
+    from callfs_amd.device import Plan
+    sb = _batch(4, 2, 4096, 2, seed=3)
+    p = Plan.for_batch(sb)
+    assert N.lib.rs_plan_tune(p.handle, None, 0, None, 0) == N.RS_E_ARG        # reps < 1
+    assert N.lib.rs_plan_tune(p.handle, None, 1, None, 2) == N.RS_E_ARG        # no array
+    assert N.lib.rs_plan_tune(None, None, 1, None, 0) == N.RS_E_ARG
+    out = (ctypes.c_int * 3)(-7, -7, -7)
+    assert N.lib.rs_plan_tune(p.handle, None, 1, out, 3) == 0
+    assert out[0] in range(5) and out[1] == -1 and out[2] == -1

@@ -19,6 +19,17 @@ __device__ __forceinline__ void op(uint32_t& a, uint32_t b, uint32_t c) {
     asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a) : "v"(b), "v"(c));
   if constexpr (OP == 4) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
   if constexpr (OP == 5) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(a));
+  // byte select + OR (the LDS kernel's table address): SDWA with VGPR / SGPR base
+  if constexpr (OP == 6)
+    asm volatile("v_or_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+                 : "+v"(a) : "v"(b));
+  if constexpr (OP == 7)
+    asm volatile("v_or_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+                 : "+v"(a) : "s"(b));
+  if constexpr (OP == 8) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+  if constexpr (OP == 9) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(b));
+  if constexpr (OP == 10) asm volatile("v_lshrrev_b32 %0, 8, %0" : "+v"(a));
+  if constexpr (OP == 11) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(a));
 }
 
 template <int OP>
@@ -47,11 +58,13 @@ int main() {
   const int blocks = 256 * 8;  // 8 blocks of 4 waves per CU = 8 waves per SIMD
   const int iters = 2000;
   const char* names[] = {"v_add_u32", "v_perm_b32", "v_alignbit_b32 (vgpr shift)", "v_bitop3_b32",
-                         "v_add3_u32", "v_alignbit_b32 (rotate imm)"};
+                         "v_add3_u32", "v_alignbit_b32 (rotate imm)", "v_or_b32_sdwa (vgpr)",
+                         "v_or_b32_sdwa (sgpr)", "v_and_or_b32", "v_xor_b32", "v_lshrrev_b32",
+                         "v_bfe_u32"};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int opi = 0; opi < 6; ++opi) {
+  for (int opi = 0; opi < 12; ++opi) {
     auto launch = [&]() {
       switch (opi) {
         case 0: hipLaunchKernelGGL(valu_kernel<0>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
@@ -60,6 +73,12 @@ int main() {
         case 3: hipLaunchKernelGGL(valu_kernel<3>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
         case 4: hipLaunchKernelGGL(valu_kernel<4>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
         case 5: hipLaunchKernelGGL(valu_kernel<5>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
+        case 6: hipLaunchKernelGGL(valu_kernel<6>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
+        case 7: hipLaunchKernelGGL(valu_kernel<7>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
+        case 8: hipLaunchKernelGGL(valu_kernel<8>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
+        case 9: hipLaunchKernelGGL(valu_kernel<9>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
+        case 10: hipLaunchKernelGGL(valu_kernel<10>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
+        case 11: hipLaunchKernelGGL(valu_kernel<11>, dim3(blocks), dim3(256), 0, 0, out, iters, 5u); break;
       }
     };
     launch();
