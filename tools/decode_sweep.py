@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--patterns", default="enc;;5;0,3,7,12;0,1,2,3;10,11,12,13;0;13")
+    ap.add_argument("--tune", type=int, default=0,
+                    help="1: also time a second plan per pattern tuned by rs_plan_tune")
     a = ap.parse_args()
     k, m, S, B = a.k, a.m, a.shard_bytes, a.stripes
     dev = torch.device("cuda", 0)
@@ -42,13 +44,21 @@ def main():
     enc = Plan.for_batch(sb)
     enc.launch(stream)  # consistent parity: verify rows must pass
     plans = []
+    orders = {}
     for p in a.patterns.split(";"):
         if p == "enc":
             plans.append(("encode", enc))
-            continue
-        erase = sorted({int(x) for x in p.split(",") if x})
-        present = [i not in erase for i in range(k + m)]
-        plans.append((f"decode erase {erase}", Plan.for_batch(sb, present=present)))
+            present = None
+            name = "encode"
+        else:
+            erase = sorted({int(x) for x in p.split(",") if x})
+            present = [i not in erase for i in range(k + m)]
+            name = f"decode erase {erase}"
+            plans.append((name, Plan.for_batch(sb, present=present)))
+        if a.tune:
+            tuned = Plan.for_batch(sb, present=present)
+            orders[name + " (tuned)"] = tuned.tune(stream=stream)
+            plans.append((name + " (tuned)", tuned))
     times = {name: [] for name, _ in plans}
     for rd in range(a.rounds):
         for j in range(len(plans)):
@@ -69,7 +79,8 @@ def main():
         print(json.dumps({"k": k, "m": m, "S": S, "stripes": B, "plan": name,
                           "bytes_per_launch": pl.bytes, "median_ms": round(med, 4),
                           "GB/s": round(gbs, 1), "frac_8TBs": round(gbs / 8000, 4),
-                          "object_GiB/s": round(B * k * S / (med * 1e-3) / 2**30, 1)}))
+                          "object_GiB/s": round(B * k * S / (med * 1e-3) / 2**30, 1),
+                          "tile_order": orders.get(name)}))
 
 
 if __name__ == "__main__":
