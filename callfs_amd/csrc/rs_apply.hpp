@@ -97,14 +97,17 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //            global_load_dwordx4
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
           int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, bool REALIGN_ = false,
-          bool SDWA_ = false>
+          bool SDWA_ = false, int PROBE_ = 0>
 struct Policy {
+  // tools/kbench layout probes (never dispatched): 1 = 63-vector waves (the REALIGN
+  // tiling) with plain loads, lane 63 idle; 2 = 64-vector waves, lane 63 idle
+  static constexpr int PROBE = PROBE_;
   static constexpr bool NOMATH = NOMATH_;
   // LDS table addresses by v_or_b32_sdwa (byte select + OR) instead of v_perm_b32
   static constexpr bool SDWA = SDWA_;
   static constexpr bool REALIGN = REALIGN_;
   // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads
-  static constexpr int TILE_VECS = REALIGN_ ? BS_ / 64 * 63 : BS_ * U_;
+  static constexpr int TILE_VECS = (REALIGN_ || PROBE_ == 1) ? BS_ / 64 * 63 : BS_ * U_;
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
   static constexpr bool NT_LOAD = NT_LOAD_;
@@ -166,8 +169,18 @@ __device__ __forceinline__ void mac_one(uint32_t (&acc)[U][RT][4], const uint4 (
     }
 }
 
-// The ragged tail S % 16 of every shard, run by the stripe's last tile of the v_perm
-// kernel (one byte per thread): odd-S launches need no second kernel.
+// The ragged tail S % 16 of every shard, run by the stripe's first tile of the v_perm
+// kernel (one byte per thread): odd-S launches need no second kernel. The first tile, not
+// the last: the tail is a chain of K byte loads, and in the stripe's last tile (the
+// grid's last for the last stripe) it outlasted the other waves and delayed the kernel's
+// end by ~2 %. Loads are issued kTailLoads at a time.
+constexpr int kTailLoads = 4;
+template <int RT>
+__device__ __forceinline__ void tail_bytes(cptr<const uint8_t*> in, uint64_t b, int i0, int K,
+                                           uint32_t (&x)[kTailLoads]) {
+#pragma unroll
+  for (int j = 0; j < kTailLoads; ++j) x[j] = i0 + j < K ? in[i0 + j][b] : 0u;
+}
 template <int RT>
 __device__ __forceinline__ void vec_tail(const ApplyArgs& a, cptr<const uint8_t*> in,
                                          cptr<uint8_t*> out, uint32_t stripe,
@@ -178,11 +191,15 @@ __device__ __forceinline__ void vec_tail(const ApplyArgs& a, cptr<const uint8_t*
   uint32_t acc[RT];
 #pragma unroll
   for (int r = 0; r < RT; ++r) acc[r] = 0;
-  for (int i = 0; i < a.K; ++i) {
-    const Sel sel = selectors(in[i][b]);
-    const cptr<uint32_t> t = tabs + static_cast<size_t>(i) * RT * 5;
+  for (int i0 = 0; i0 < a.K; i0 += kTailLoads) {
+    uint32_t x[kTailLoads];
+    tail_bytes<RT>(in, b, i0, a.K, x);
+    for (int j = 0; j < kTailLoads && i0 + j < a.K; ++j) {
+      const Sel sel = selectors(x[j]);
+      const cptr<uint32_t> t = tabs + static_cast<size_t>(i0 + j) * RT * 5;
 #pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r] = fma1(acc[r], gf_mul4(sel, t + r * 5));
+      for (int r = 0; r < RT; ++r) acc[r] = fma1(acc[r], gf_mul4(sel, t + r * 5));
+    }
   }
   bool bad = false;
 #pragma unroll
@@ -220,7 +237,7 @@ void rs_apply_vec(ApplyArgs a) {
     const uint64_t v0 = static_cast<uint64_t>(tile) * tile_vecs + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * RT;
-    if (tile == tps - 1 && a.tail_in_vec) vec_tail<RT>(a, in, out, stripe, tabs);
+    if (tile == 0 && a.tail_in_vec) vec_tail<RT>(a, in, out, stripe, tabs);
     bool live[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) live[u] = v0 + static_cast<uint64_t>(u) * BS < a.nvec;
@@ -526,8 +543,9 @@ __device__ __forceinline__ uint32_t lds_byte(const typename LdsAcc<RT>::T& t, in
   else return static_cast<uint32_t>(t >> (8 * r)) & 0xffu;
 }
 
-// The ragged tail S % 16 of every shard, run by the stripe's last tile (one byte per
-// thread, the same LDS tables), so that launches with odd S need no second kernel
+// The ragged tail S % 16 of every shard, run by the stripe's first tile (one byte per
+// thread, the same LDS tables; first, not last: see vec_tail), so that launches with odd
+// S need no second kernel
 // (launch_apply sets ApplyArgs::tail_in_vec). Entry e of input i's low / high table is
 // at lds0 + 32*W*i + W*e / + 16*W + W*e.
 template <int RT>
@@ -538,10 +556,14 @@ __device__ __forceinline__ void lds_tail(const ApplyArgs& a, cptr<const uint8_t*
   if (threadIdx.x >= nt) return;
   const uint64_t b = a.nvec * 16 + threadIdx.x;
   typename LdsAcc<RT>::T t = lds_zero<RT>();
-  for (int i = 0; i < a.K; ++i) {
-    const uint32_t x = in[i][b];
-    const uint32_t base = lds0 + static_cast<uint32_t>(i) * 32u * W;
-    t = t ^ lds_lookup<RT>(base + (x & 15u) * W) ^ lds_lookup<RT>(base + 16u * W + (x >> 4) * W);
+  for (int i0 = 0; i0 < a.K; i0 += kTailLoads) {
+    uint32_t x[kTailLoads];
+    tail_bytes<RT>(in, b, i0, a.K, x);
+    for (int j = 0; j < kTailLoads && i0 + j < a.K; ++j) {
+      const uint32_t base = lds0 + static_cast<uint32_t>(i0 + j) * 32u * W;
+      t = t ^ lds_lookup<RT>(base + (x[j] & 15u) * W) ^
+          lds_lookup<RT>(base + 16u * W + (x[j] >> 4) * W);
+    }
   }
   bool bad = false;
   for (int r = 0; r < a.R && r < RT; ++r) {
@@ -588,13 +610,14 @@ void rs_apply_lds(ApplyArgs a) {
     map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
     // REALIGN: wave w of the tile produces vectors tile*TV + 63w + lane (lanes 0..62)
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t v0 = P::REALIGN ? static_cast<uint64_t>(tile) * TV + (threadIdx.x >> 6) * 63u + lane
-                                   : static_cast<uint64_t>(tile) * BS + threadIdx.x;
+    const uint64_t v0 = (P::REALIGN || P::PROBE == 1)
+                            ? static_cast<uint64_t>(tile) * TV + (threadIdx.x >> 6) * 63u + lane
+                            : static_cast<uint64_t>(tile) * BS + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
-    if (tile == tps - 1 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
+    if (tile == 0 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
     // lanes that store (REALIGN: lane 63 and lanes past the shard only load)
-    const bool active = v0 < a.nvec && (!P::REALIGN || lane != 63u);
+    const bool active = v0 < a.nvec && (!(P::REALIGN || P::PROBE) || lane != 63u);
     if (P::REALIGN ? (v0 - lane >= a.nvec) : !active) continue;  // REALIGN: whole wave idle
     auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
     AccT acc[4][4];

@@ -250,7 +250,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
     tail0 = a.nvec * 16;
     if (a.nvec) {
       if (takes_lds(a)) {
-        // the LDS kernel's last tile per stripe computes the S % 16 tail itself: an odd-S
+        // the LDS kernel's first tile per stripe computes the S % 16 tail itself: an odd-S
         // launch (Split layout) is one kernel, not two back to back
         a.tail_in_vec = tail0 < a.S;
         if (a.tail_in_vec) tail0 = a.S;
@@ -291,7 +291,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, a);
         });
       } else {
-        a.tail_in_vec = tail0 < a.S;  // as for the LDS kernel: the last tile takes the tail
+        a.tail_in_vec = tail0 < a.S;  // as for the LDS kernel: the first tile takes the tail
         if (a.tail_in_vec) tail0 = a.S;
         VecFn fn = kVec[a.R - 1];  // R <= 4 here (R >= kLdsMinRows takes the LDS kernel)
         switch (order >= 0 ? static_cast<TileOrder>(order) : vec_rule(a)) {

@@ -42,7 +42,7 @@ struct ApplyArgs {
   // some input shard is not 16-B aligned (upstream Split layout of a contiguous object
   // at odd S); selects the LDS kernel's realigning form (rs_apply.hpp REALIGN)
   uint32_t in_misalign;
-  // set by launch_apply: the vector kernel's last tile per stripe also computes the ragged
+  // set by launch_apply: the vector kernel's first tile per stripe also computes the ragged
   // tail S % 16 (no separate byte-kernel launch)
   uint32_t tail_in_vec;
 };

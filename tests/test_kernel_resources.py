@@ -34,6 +34,11 @@ def kernels():
     return ks
 
 
+def _policy(k):
+    """The Policy<...> template arguments of a kernel's name."""
+    return [x.strip() for x in re.search(r"Policy<([^>]*)>", k["name"]).group(1).split(",")]
+
+
 def _lds(ks):
     return [k for k in ks if "rs_apply_lds<" in k["name"]]
 
@@ -60,7 +65,7 @@ def test_lds_kernel_occupancy(kernels):
     (16-byte entries): 4 waves."""
     for k in _lds(kernels):
         r = int(re.search(r"rs_apply_lds<(\d+),", k["name"]).group(1))
-        realign = re.search(r"Policy<([^>]*)>", k["name"]).group(1).split(",")[10].strip() == "true"
+        realign = _policy(k)[10] == "true"
         want = 8 if r <= 4 else (6 if realign else 7) if r <= 8 else 4
         assert k["waves_per_simd"] >= want, (k["name"], k["vgprs"], k["waves_per_simd"])
         if r > 8:
@@ -68,9 +73,8 @@ def test_lds_kernel_occupancy(kernels):
 
 
 def test_wide_groups_use_sdwa_addresses(kernels):
-    """The production R 9..16 policies carry the SDWA flag (last Policy argument)."""
+    """The production R 9..16 policies carry the SDWA flag (12th Policy argument)."""
     wide = [k for k in _lds(kernels) if int(re.search(r"rs_apply_lds<(\d+),", k["name"]).group(1)) > 8]
     assert len(wide) >= 16
     for k in wide:
-        args = re.search(r"Policy<([^>]*)>", k["name"]).group(1).split(",")
-        assert args[-1].strip() == "true", k["name"]
+        assert _policy(k)[11] == "true", k["name"]  # Policy::SDWA

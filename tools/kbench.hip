@@ -470,6 +470,28 @@ int main(int argc, char** argv) {
     vs.push_back(Variant{"prod dispatch (2nd)", [](const ApplyArgs& a, hipStream_t s) {
                            CK(launch_apply(a, s));
                          }});
+  if (std::getenv("KB_PROBE63") && m <= 8) {  // wave-tiling probes (lane 63 idle; parity incomplete)
+    static void (*const p1[8])(const ApplyArgs&, hipStream_t) = {
+#define KB_P(R) [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, Policy<2, 1, true, true, false, 512, 2, 0, 0, false, false, false, 1>>(a, s); }
+        KB_P(1), KB_P(2), KB_P(3), KB_P(4), KB_P(5), KB_P(6), KB_P(7), KB_P(8)};
+#undef KB_P
+    static void (*const p2[8])(const ApplyArgs&, hipStream_t) = {
+#define KB_P(R) [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, Policy<2, 1, true, true, false, 512, 2, 0, 0, false, false, false, 2>>(a, s); }
+        KB_P(1), KB_P(2), KB_P(3), KB_P(4), KB_P(5), KB_P(6), KB_P(7), KB_P(8)};
+#undef KB_P
+    static void (*const rc[8])(const ApplyArgs&, hipStream_t) = {
+#define KB_P(R) [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, Policy<2, 1, true, true, false, 512, 2, 0, 0, false, true>>(a, s); }
+        KB_P(1), KB_P(2), KB_P(3), KB_P(4), KB_P(5), KB_P(6), KB_P(7), KB_P(8)};
+#undef KB_P
+    vs.push_back(Variant{"probe 63-vec waves", [m](const ApplyArgs& a, hipStream_t s) { p1[m - 1](a, s); }, false});
+    vs.push_back(Variant{"probe 64-vec waves lane63 idle", [m](const ApplyArgs& a, hipStream_t s) { p2[m - 1](a, s); }, false});
+    vs.push_back(Variant{"realign consec", [m](const ApplyArgs& a, hipStream_t s) { rc[m - 1](a, s); }});
+    vs.push_back(Variant{"plain consec", [m](const ApplyArgs& a, hipStream_t s) {
+                           if (m == 4) launch_lds<4, Policy<2, 1, true, true, false, 512, 2, 0>>(a, s);
+                           else if (m == 8) launch_lds<8, Policy<2, 1, true, true, false, 512, 2, 0>>(a, s);
+                           else if (m == 2) launch_lds<2, Policy<2, 1, true, true, false, 512, 2, 0>>(a, s);
+                         }});
+  }
   {  // memory ceiling of this traffic shape: the LDS kernel's loads/stores/grid, no lookups
     static void (*const nomath_g2[16])(const ApplyArgs&, hipStream_t) = {
 #define KB_NM(R) [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, Policy<2, 1, true, true, false, 512, (R > 8 ? 4 : 2), 5, (R > 8 ? 1 : 0), true>>(a, s); }
@@ -550,10 +572,23 @@ int main(int argc, char** argv) {
     // ~3 % slow when it always went first
     for (size_t vj = 0; vj < vs.size(); ++vj) {
       const size_t vi = (vj + rd) % vs.size();
-      // warm: 4 launches (with 2, the variant timed right after a ceiling kernel's
-      // parity restore -- 256 small synchronous copies -- ran ~1.5 points slow on
-      // every shape: the clock had not come back up)
-      for (int w = 0; w < 4; ++w) vs[vi].launch(a, s);
+      // warm for >= 30 ms, not a fixed count: the variant timed right after a no-lookup
+      // ceiling kernel (light on VALU and LDS) ran 1.5-3 points slow on every shape
+      // even after 4 warm launches (profiles/r02/prod_gap/, tail_check/) -- the clock
+      // and power state of a light kernel carry over into the next one for milliseconds
+      {
+        float warm_ms = 0;
+        for (int w = 0; w < 400 && warm_ms < 30.0f; w += 2) {
+          CK(hipEventRecord(e0, s));
+          vs[vi].launch(a, s);
+          vs[vi].launch(a, s);
+          CK(hipEventRecord(e1, s));
+          CK(hipEventSynchronize(e1));
+          float t = 0;
+          CK(hipEventElapsedTime(&t, e0, e1));
+          warm_ms += t;
+        }
+      }
       CK(hipEventRecord(e0, s));
       for (int it = 0; it < iters; ++it) vs[vi].launch(a, s);
       CK(hipEventRecord(e1, s));
@@ -572,9 +607,7 @@ int main(int argc, char** argv) {
         }
       }
       // restore parity clobbered by ceiling kernels: needed for the round-0 parity checks
-      // and for Verify runs; skipped otherwise, because the variant timed right after the
-      // 256 small synchronous copies ran ~2 points slow on every shape even after 4 warm
-      // launches (tools/prod_gap_probe.sh, profiles/r02/prod_gap/)
+      // and for Verify runs (timing does not depend on the parity's contents)
       if (!vs[vi].check && vs[vi].name.rfind("probe", 0) != 0 && (rd == 0 || vmask)) {
         for (int b = 0; b < B; ++b)
           CK(hipMemcpy(out[b * m], ref + static_cast<size_t>(b) * m * opitch, m * opitch, hipMemcpyDeviceToDevice));

@@ -1,5 +1,5 @@
 set -o pipefail
-R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/pd_r02a"; mkdir -p "$OUT"
+R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/${1:-pd}"; mkdir -p "$OUT"
 export KB_SDWA=1 KB_PROD2=1
 for keep in "sdwa|perm|prod dispatch (2nd)" "sdwa|perm|prod dispatch (2nd)|nomath g2"; do
   export KB_KEEP="$keep"
