@@ -96,7 +96,7 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //            vector by DPP wave_shl:1, v_alignbyte funnel shift) instead of unaligned
 //            global_load_dwordx4
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
-          int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, bool REALIGN_ = false,
+          int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, int REALIGN_ = 0,
           bool SDWA_ = false, int PROBE_ = 0>
 struct Policy {
   // tools/kbench layout probes (never dispatched): 1 = 63-vector waves (the REALIGN
@@ -105,9 +105,12 @@ struct Policy {
   static constexpr bool NOMATH = NOMATH_;
   // LDS table addresses by v_or_b32_sdwa (byte select + OR) instead of v_perm_b32
   static constexpr bool SDWA = SDWA_;
-  static constexpr bool REALIGN = REALIGN_;
+  // 0: plain; 1: aligned loads realigned in registers (63 vectors per wave); 2: loads and
+  // parity stores both aligned (62 vectors per wave, edge bytes in the first tile)
+  static constexpr int REALIGN = REALIGN_;
   // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads
-  static constexpr int TILE_VECS = (REALIGN_ || PROBE_ == 1) ? BS_ / 64 * 63 : BS_ * U_;
+  static constexpr int WAVE_VECS = REALIGN_ == 2 ? 62 : (REALIGN_ || PROBE_ == 1) ? 63 : 64;
+  static constexpr int TILE_VECS = WAVE_VECS < 64 ? BS_ / 64 * WAVE_VECS : BS_ * U_;
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
   static constexpr bool NT_LOAD = NT_LOAD_;
@@ -353,10 +356,9 @@ __device__ __forceinline__ uint4 ld_aligned(const uint8_t* p, uint64_t v, uint64
   return load16<P>(reinterpret_cast<const uint4*>(p - d) + (v < vmax ? v : vmax));
 }
 
-// Vector v of shard p from this lane's aligned A[v] and the next lane's A[v+1]; every
-// lane of the wave executes this (lane 63's result is not used).
-__device__ __forceinline__ uint4 realign(const uint8_t* p, const uint4& A) {
-  const uint32_t d = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u;
+// Bytes d..15 of this lane's A followed by bytes 0..d-1 of the next lane's A (d
+// wave-uniform); every lane of the wave executes this (lane 63's result is not used).
+__device__ __forceinline__ uint4 shift_from_next(const uint4& A, uint32_t d) {
   if (d == 0) return A;  // wave-uniform
   const uint4 B = make_uint4(from_next_lane(A.x), from_next_lane(A.y), from_next_lane(A.z),
                              from_next_lane(A.w));
@@ -368,6 +370,20 @@ __device__ __forceinline__ uint4 realign(const uint8_t* p, const uint4& A) {
     default: return funnel16<3>(A, B, r);
   }
 }
+
+// Vector v of shard p from this lane's aligned A[v] and the next lane's A[v+1].
+__device__ __forceinline__ uint4 realign(const uint8_t* p, const uint4& A) {
+  return shift_from_next(A, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u);
+}
+
+// ---- aligned parity stores of misaligned rows (Policy::REALIGN == 2) -----------------
+// Row q with mo = q & 15 != 0 and f = 16 - mo: the aligned 16-B block at q + f + 16v holds
+// bytes f..15 of result vector v and bytes 0..f-1 of vector v+1, so lane l stores
+// shift_from_next(R[v0], f) there for v0 <= nvec - 2. A wave computes 63 valid results
+// (lanes 0..62, REALIGN loads) and stores 62 blocks (lanes 0..61); the next wave starts
+// at the 62nd. Each stripe's first tile writes the bytes no aligned block covers, one
+// byte per thread (lds_edges): the head [0, f) and the tail [16(nvec-1) + f, S) of every
+// misaligned row, [16 nvec, S) of aligned rows and Verify rows.
 
 // ---- LDS nibble-table variant ---------------------------------------------------------
 // Per data byte two LDS lookups (low / high nibble) return the products for all RT rows
@@ -574,6 +590,42 @@ __device__ __forceinline__ void lds_tail(const ApplyArgs& a, cptr<const uint8_t*
   if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
 }
 
+// Edge bytes of a REALIGN == 2 launch (see "aligned parity stores" above); threads
+// 0..15 take the head bytes 0..15, threads 16.. the bytes from 16 (nvec - 1) on.
+template <int RT>
+__device__ __forceinline__ void lds_edges(const ApplyArgs& a, cptr<const uint8_t*> in,
+                                          cptr<uint8_t*> out, uint32_t stripe, uint32_t lds0) {
+  constexpr int W = LdsAcc<RT>::W;
+  const uint64_t t0 = a.nvec * 16 - 16;  // nvec >= 1 on this path
+  const uint32_t j = threadIdx.x;
+  const bool head = j < 16u;
+  const uint64_t b = head ? j : t0 + (j - 16u);
+  if (!head && b >= a.S) return;
+  if (head && b >= a.S) return;
+  typename LdsAcc<RT>::T t = lds_zero<RT>();
+  for (int i0 = 0; i0 < a.K; i0 += kTailLoads) {
+    uint32_t x[kTailLoads];
+    tail_bytes<RT>(in, b, i0, a.K, x);
+    for (int jj = 0; jj < kTailLoads && i0 + jj < a.K; ++jj) {
+      const uint32_t base = lds0 + static_cast<uint32_t>(i0 + jj) * 32u * W;
+      t = t ^ lds_lookup<RT>(base + (x[jj] & 15u) * W) ^
+          lds_lookup<RT>(base + 16u * W + (x[jj] >> 4) * W);
+    }
+  }
+  bool bad = false;
+  for (int r = 0; r < a.R && r < RT; ++r) {
+    const uint8_t v = static_cast<uint8_t>(lds_byte<RT>(t, r));
+    const bool verify = (a.verify_mask >> r) & 1u;
+    const uint32_t f = (16u - (static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r])) & 15u)) & 15u;
+    const bool mine = head ? (!verify && b < f)
+                           : (verify || f == 0) ? b >= a.nvec * 16 : b >= t0 + f;
+    if (!mine) continue;
+    if (verify) bad |= out[r][b] != v;
+    else out[r][b] = v;
+  }
+  if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
+}
+
 // Waves per SIMD the LDS kernel may be limited to: 16-byte entries keep 8 b128 reads
 // (32 VGPRs) in flight, which the register allocator only grants below 5 waves.
 template <int RT>
@@ -610,14 +662,19 @@ void rs_apply_lds(ApplyArgs a) {
     map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
     // REALIGN: wave w of the tile produces vectors tile*TV + 63w + lane (lanes 0..62)
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t v0 = (P::REALIGN || P::PROBE == 1)
-                            ? static_cast<uint64_t>(tile) * TV + (threadIdx.x >> 6) * 63u + lane
-                            : static_cast<uint64_t>(tile) * BS + threadIdx.x;
+    constexpr uint32_t WV = P::WAVE_VECS;
+    const uint64_t v0 = WV < 64 ? static_cast<uint64_t>(tile) * TV + (threadIdx.x >> 6) * WV + lane
+                                : static_cast<uint64_t>(tile) * BS + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
-    if (tile == 0 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
-    // lanes that store (REALIGN: lane 63 and lanes past the shard only load)
-    const bool active = v0 < a.nvec && (!(P::REALIGN || P::PROBE) || lane != 63u);
+    if constexpr (P::REALIGN == 2) {
+      if (tile == 0) lds_edges<RT>(a, in, out, stripe, lds0);
+    } else {
+      if (tile == 0 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
+    }
+    // lanes that store (REALIGN: lane 63 -- REALIGN 2: lanes 62, 63 -- and lanes past the
+    // shard only load)
+    const bool active = v0 < a.nvec && lane < WV && !(P::PROBE == 2 && lane == 63u);
     if (P::REALIGN ? (v0 - lane >= a.nvec) : !active) continue;  // REALIGN: whole wave idle
     auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
     AccT acc[4][4];
@@ -684,6 +741,18 @@ void rs_apply_lds(ApplyArgs a) {
       const uint4 o = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
                                  lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
       uint4* dst = reinterpret_cast<uint4*>(out[r]) + v0;
+      if constexpr (P::REALIGN == 2) {
+        if (!((a.verify_mask >> r) & 1u)) {
+          const uint32_t mo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r])) & 15u;
+          if (mo) {  // wave-uniform: aligned block at out[r] + f + 16 v0 (see above)
+            const uint32_t f = 16u - mo;
+            const uint4 O = shift_from_next(o, f);  // every lane: DPP reads lane + 1
+            if (active && v0 + 1 < a.nvec)
+              store16<P>(reinterpret_cast<uint4*>(out[r] + f) + v0, O);
+            continue;
+          }
+        }
+      }
       if (P::REALIGN && !active) continue;
       if ((a.verify_mask >> r) & 1u) {
         const uint4 y = *dst;

@@ -204,6 +204,7 @@ struct LayoutHint {
   int addr_tz = 0;
   uint64_t stripe_stride = 0;
   uint32_t in_misalign = 0;
+  uint32_t out_misalign = 0;  // over every launch group's output pointers
 };
 
 // One pipeline stage of the host-memory path: a stream, a pinned chunk buffer and its
@@ -291,7 +292,7 @@ template <class F>
 LayoutHint fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h, F shard_ptr) {
   std::memset(h + L.status_off, 0, sizeof(int) * static_cast<size_t>(batch));
   auto* in = reinterpret_cast<const uint8_t**>(h + L.in_off);
-  uint32_t misalign = 0;
+  uint32_t misalign = 0, out_misalign = 0;
   for (int b = 0; b < batch; ++b)
     for (int i = 0; i < t.k; ++i) {
       const uint8_t* p = shard_ptr(b, t.valid[i]);
@@ -303,7 +304,10 @@ LayoutHint fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h
     auto* out = reinterpret_cast<uint8_t**>(h + L.out_off[gi]);
     const size_t R = g.shard.size();
     for (int b = 0; b < batch; ++b)
-      for (size_t r = 0; r < R; ++r) out[b * R + r] = const_cast<uint8_t*>(shard_ptr(b, g.shard[r]));
+      for (size_t r = 0; r < R; ++r) {
+        out[b * R + r] = const_cast<uint8_t*>(shard_ptr(b, g.shard[r]));
+        out_misalign |= static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[b * R + r])) & 15u;
+      }
     std::memcpy(h + L.tab_off[gi], g.tabs.data(), g.tabs.size() * sizeof(uint32_t));
     std::memcpy(h + L.ltab_off[gi], g.ltabs.data(), g.ltabs.size());
   }
@@ -313,6 +317,7 @@ LayoutHint fill_meta(const Tables& t, const MetaLayout& L, int batch, uint8_t* h
     for (int i : g.shard) s0.push_back(shard_ptr(0, i));
   LayoutHint hint;
   hint.in_misalign = misalign;
+  hint.out_misalign = out_misalign;
   hint.addr_tz = shard_addr_tz(s0.data(), static_cast<int>(s0.size()));
   if (batch > 1) {
     const int v = t.valid[0];
@@ -343,6 +348,7 @@ ApplyArgs group_args(const Tables& t, const MetaLayout& L, size_t gi, int batch,
   a.addr_tz = hint.addr_tz;
   a.stripe_stride = hint.stripe_stride;
   a.in_misalign = hint.in_misalign;
+  a.out_misalign = hint.out_misalign;
   return a;
 }
 

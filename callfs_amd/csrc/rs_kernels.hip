@@ -56,15 +56,23 @@ using LdsG8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 2>;
 using LdsG2Policy = dev::Policy<2, 1, true, true, false, 512, 2, 5>;
 using LdsQ8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 6>;
 using LdsQ16Policy = dev::Policy<2, 1, true, true, false, 512, 2, 8>;
-// Misaligned input shards with k >= 8 and R <= 8: aligned loads realigned in registers,
-// 63 vectors per wave, consecutive tiles (rs_apply.hpp REALIGN; tools/realign_sweep.sh,
-// profiles/r02/realign/, % of 8 TB/s, unaligned loads -> realigned): RS(10,4) 64 MiB
-// objects in the Split layout (S = 6,710,887) 66.5 -> 70.7, with aligned parity 68.5 ->
-// 72.7; RS(10,8) 1,048,577 B 63.6 -> 65.9; RS(16,4) 262,145 B 65.1 -> 66.2; RS(10,4)
-// 1,048,577 B 68.9 -> 69.8. With few inputs it loses (RS(4,2) 68.8 -> 67.4), and aligned
-// shards keep the plain kernel (the 504-vector tile costs 5 points there).
-using LdsRealignPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0, 0, false, true>;
-constexpr int kRealignMinK = 8;
+// Misaligned shards (upstream Split layout of contiguous objects at odd S) with R <= 8:
+// loads from aligned addresses realigned in registers, and parity stores to aligned
+// addresses realigned the same way (62 vectors per wave; the bytes no aligned block
+// covers are written by each stripe's first tile; rs_apply.hpp REALIGN 2). Round 1's
+// form realigned only the loads (REALIGN 1, 63 vectors per wave, k >= 8; kept in
+// tools/kbench for comparison). tools/realign_out_sweep.sh, tools/wave_tiling_probe.sh,
+// profiles/r02/realign_out/, % of 8 TB/s, unaligned -> loads realigned -> loads and stores
+// realigned: RS(10,4) 64 MiB objects (S = 6,710,887) 67.6 -> 68.1 -> 69.5, RS(10,8)
+// 1,048,577 B 63.9 -> 65.3 -> 67.0, RS(6,3) 65.6 -> 67.0 -> 71.5, RS(5,3) 68.7 -> 66.7
+// -> 72.2, RS(4,2) 69.0 -> 69.1 -> 69.8; RS(12,4) S = 5,592,406 ran 71.2 unaligned and
+// 68.9 realigned, so rs_plan_tune offers the unaligned kernel as an alternative.
+// (R <= 4 asks for 8 waves per SIMD: left alone the compiler used 106 SGPRs, 7 waves)
+using LdsRealignOutPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0, 0, false, 2>;
+using LdsRealignOut8Policy = dev::Policy<8, 1, true, true, false, 512, 2, 0, 0, false, 2>;
+template <int R>
+using LdsRealignOutPolicyFor =
+    typename std::conditional<(R <= 4), LdsRealignOut8Policy, LdsRealignOutPolicy>::type;
 // CALLFS_RS_TILE_ORDER=consecutive|g8|g2|q8|q16 overrides the rule for every LDS-kernel
 // launch with R <= 8 (A/B on a deployment's own shard layout; unset = the rule).
 int tile_order_override() {
@@ -166,7 +174,11 @@ const auto kLdsG8 = lds_order_table<LdsG8Policy>(std::make_integer_sequence<int,
 const auto kLdsG2 = lds_order_table<LdsG2Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ8 = lds_order_table<LdsQ8Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ16 = lds_order_table<LdsQ16Policy>(std::make_integer_sequence<int, 8>{});
-const auto kLdsRealign = lds_order_table<LdsRealignPolicy>(std::make_integer_sequence<int, 8>{});
+template <int... Rs>
+constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1>>...};
+}
+const auto kLdsRealignOut = lds_realign_out_table(std::make_integer_sequence<int, 8>{});
 template <class P, int... Rs>
 constexpr auto lds_wide_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 9, P>...};
@@ -197,9 +209,27 @@ TileOrder vec_rule(const ApplyArgs& a) {
   return vec_tile_order(a.S, (a.nvec + ProdPolicy::BS - 1) / ProdPolicy::BS, a.addr_tz);
 }
 
+// CALLFS_RS_REALIGN=0 sends misaligned launches to the plain kernel (unaligned 16-B
+// loads and stores; A/B)
+bool realign_out_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CALLFS_RS_REALIGN");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 bool takes_lds(const ApplyArgs& a) { return a.R >= kLdsMinRows || a.K >= kLdsMinK; }
+// Misaligned R <= 8 launches can take the realigning kernel; by default they do when some
+// shard sits at an odd byte offset. Shards misaligned only by even offsets (even S) ran
+// the plain kernel 2.3-4.3 points faster (RS(12,4), S = 5,592,406, two boxes), odd ones
+// mostly slower (RS(6,3) -6, RS(5,3) -4, RS(10,8) -1.7; RS(10,4) and RS(4,2) within
+// +-1.4 depending on the box). rs_plan_tune times both.
+bool can_realign(const ApplyArgs& a) {
+  return a.R <= 8 && (a.in_misalign || a.out_misalign) && realign_out_enabled();
+}
 bool takes_realign(const ApplyArgs& a) {
-  return a.R <= 8 && a.in_misalign && a.K >= kRealignMinK;
+  return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u);
 }
 
 }  // namespace
@@ -221,8 +251,9 @@ std::vector<int> order_candidates(const ApplyArgs& a0) {
       add(TileOrder::kSeg8);
       return c;
     }
-    if (takes_realign(a)) return c;
+    if (takes_realign(a)) add(static_cast<TileOrder>(kOrderRealign));
     add(lds_rule(a));
+    if (can_realign(a)) add(static_cast<TileOrder>(kOrderRealign));
     add(TileOrder::kConsecutive);
     add(TileOrder::kGroup2);
     if (tps <= 32) add(TileOrder::kGroup8);
@@ -258,7 +289,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
-          switch (order >= 0 ? static_cast<TileOrder>(order) : lds_rule(a)) {
+          switch (order >= 0 && order != kOrderRealign ? static_cast<TileOrder>(order) : lds_rule(a)) {
             case TileOrder::kGroup8: fn = kLdsG8[a.R - 1]; break;
             case TileOrder::kGroup2: fn = kLdsG2[a.R - 1]; break;
             case TileOrder::kSeg8: fn = kLdsQ8[a.R - 1]; break;
@@ -280,12 +311,17 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         static_assert(LdsPolicy::BS == LdsWidePolicy::BS && LdsPolicy::U == LdsWidePolicy::U &&
                           LdsG8Policy::BS == LdsPolicy::BS && LdsG2Policy::BS == LdsPolicy::BS &&
                           LdsQ8Policy::BS == LdsPolicy::BS && LdsQ16Policy::BS == LdsPolicy::BS &&
-                          LdsWideQ8Policy::BS == LdsPolicy::BS && LdsRealignPolicy::BS == LdsPolicy::BS,
+                          LdsWideQ8Policy::BS == LdsPolicy::BS &&
+                          LdsRealignOutPolicy::BS == LdsPolicy::BS &&
+                          LdsRealignOut8Policy::TILE_VECS == LdsRealignOutPolicy::TILE_VECS,
                       "one grid shape for every LDS policy");
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
-        if (takes_realign(a)) {
-          fn = kLdsRealign[a.R - 1];
-          gx = dev::vec_grid<LdsRealignPolicy>(a.nvec, a.batch);
+        // misaligned shards: the realigning form, unless a tuned order names a plain kernel
+        if (can_realign(a) && (order == kOrderRealign || (order < 0 && takes_realign(a)))) {
+          fn = kLdsRealignOut[a.R - 1];
+          gx = dev::vec_grid<LdsRealignOutPolicy>(a.nvec, a.batch);
+          a.tail_in_vec = 1;  // its first tile writes every edge byte, the tail included
+          tail0 = a.S;
         }
         launch_sliced(gx, a.K + a.R, a, [&](uint32_t blocks) {
           hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, a);

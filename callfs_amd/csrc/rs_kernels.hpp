@@ -42,6 +42,9 @@ struct ApplyArgs {
   // some input shard is not 16-B aligned (upstream Split layout of a contiguous object
   // at odd S); selects the LDS kernel's realigning form (rs_apply.hpp REALIGN)
   uint32_t in_misalign;
+  // the same over the launch group's output (written or compared) shard pointers; with
+  // in_misalign it selects the form that also aligns the parity stores (REALIGN 2)
+  uint32_t out_misalign;
   // set by launch_apply: the vector kernel's first tile per stripe also computes the ragged
   // tail S % 16 (no separate byte-kernel launch)
   uint32_t tail_in_vec;
@@ -62,6 +65,11 @@ inline int shard_addr_tz(const void* const* p, int count) {
 // offsets (upstream Split layout of a contiguous object) that ran 4.7x the byte kernel
 // (DESIGN.md §5). bytes_only forces the byte kernel over all of [0, S) (kbench A/B).
 // Returns hipSuccess or the launch error.
+// order_candidates / launch_apply code for the realigning kernel of misaligned launches
+// (tile orders are TileOrder values 0..4, which on a misaligned launch select the plain
+// kernel with unaligned accesses)
+constexpr int kOrderRealign = 32;
+
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the
 // rule (or CALLFS_RS_TILE_ORDER).

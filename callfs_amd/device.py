@@ -95,7 +95,9 @@ class Plan:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         N.check(N.lib.rs_plan_launch(self.handle, ctypes.c_void_p(s.cuda_stream)), "rs_plan_launch")
 
-    ORDER_NAMES = {-1: "none", 0: "consecutive", 1: "g8", 2: "g2", 3: "q8", 4: "q16"}
+    # tile orders (RS_ORDER_*); on misaligned shards 0..4 name the plain kernel with
+    # unaligned accesses and "realign" the kernel that aligns loads and stores
+    ORDER_NAMES = {-1: "none", 0: "consecutive", 1: "g8", 2: "g2", 3: "q8", 4: "q16", 32: "realign"}
 
     def tune(self, reps: int = 5, stream: Optional[torch.cuda.Stream] = None) -> list:
         """rs_plan_tune: time each launch group in every tile order its kernel offers

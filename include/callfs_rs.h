@@ -176,6 +176,10 @@ void rs_plan_destroy(rs_plan* plan);
 #define RS_ORDER_GROUP2 2
 #define RS_ORDER_SEG8 3
 #define RS_ORDER_SEG16 4
+/* misaligned shards (upstream Split layout at odd S): the kernel that realigns loads and
+ * parity stores in registers; on such launches RS_ORDER_0..4 name the plain kernel with
+ * unaligned 16-B accesses in that tile order */
+#define RS_ORDER_REALIGN 32
 int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups);
 
 /* One-shot device-resident calls (build + launch + free; tables cached per profile).

@@ -1050,12 +1050,22 @@ def test_host_pool_reuses_freed_buffers(native_lib):
     (12, 8, 4096 * 3 + 1, 5, 13),      # R = 8, odd stripe stride
     (8, 2, 16 * 504 * 2 + 15, 2, 5),   # k = 8 (the rule's minimum), 504-vector tile boundaries
     (10, 4, 1_000_003, 2, 11),         # Split layout of ~10 MB objects
+    # aligned parity stores (REALIGN 2: 62 stored vectors per wave, 496 per tile, edge
+    # bytes written by each stripe's first tile)
+    (10, 4, 32, 3, 9),                 # two vectors: one aligned block per row at most
+    (10, 4, 16 * 62 + 3, 3, 5),        # one wave's 62 stored vectors
+    (10, 4, 16 * 63 + 15, 2, 1),       # 63: the second wave stores the last block
+    (9, 6, 16 * 496 + 16 * 62 + 1, 2, 14),  # tile and wave boundaries, R = 6
+    (10, 4, 16 * 1000, 2, 3),          # S % 16 == 0, every shard misaligned by 3
+    (8, 3, 16 * 496 * 3 + 7, 2, 8),    # R = 3, three tiles
 ])
 def test_plan_misaligned_batch_realign(native_lib, k, m, S, batch, off):
     """Contiguous stripes in the upstream Split layout at odd S (every input shard at its
     own byte misalignment, odd stripe stride): k >= 8 launches take the realigning LDS
-    kernel (aligned loads, DPP + v_alignbyte, 63 vectors per wave). Encode, a decode
-    erasing m shards, and a decode with Verify rows, against the oracle per stripe."""
+    kernel (aligned loads, DPP + v_alignbyte), and with misaligned parity rows its form
+    that also aligns the stores (62 vectors per wave, edge bytes in the first tile). Encode,
+    a decode erasing m shards, and a decode with Verify rows, against the oracle per
+    stripe, every byte of every stripe."""
     import torch
     from callfs_amd.device import Plan
     n = k + m
@@ -1142,3 +1152,40 @@ def test_plan_tune_argument_errors(native_lib):
     out = (ctypes.c_int * 3)(-7, -7, -7)
     assert N.lib.rs_plan_tune(p.handle, None, 1, out, 3) == 0
     assert out[0] in range(5) and out[1] == -1 and out[2] == -1
+
+
+@pytest.mark.parametrize("k,m,S,batch,off", [(10, 4, 100_003, 3, 3), (4, 2, 65_537, 5, 1),
+                                             (12, 8, 16 * 496 + 9, 2, 6)])
+def test_plan_tune_misaligned_split_layout(native_lib, k, m, S, batch, off):
+    """On misaligned (Split-layout) shards rs_plan_tune chooses between the realigning
+    kernel and the plain kernel in several tile orders; after tuning, encode and a decode
+    with a Verify row stay bit-exact on every byte of every stripe."""
+    import torch
+    from callfs_amd.device import Plan
+    n = k + m
+    total = batch * n * S
+    buf = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device="cuda:0")
+    base = buf.data_ptr() + off
+    ptrs = [base + (b * n + i) * S for b in range(batch) for i in range(n)]
+    enc = Plan(k, m, S, batch, ptrs)
+    names = enc.tune(reps=1)
+    assert all(x in {"realign", "consecutive", "g8", "g2", "q8", "q16"} for x in names), names
+    buf[off:off + total].copy_(torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda:0"))
+    enc.launch()
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()[off:off + total].copy()
+    for b in range(batch):
+        st = host[b * n * S:(b + 1) * n * S]
+        want = cref.encode([st[i * S:(i + 1) * S] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(st[(k + j) * S:(k + j + 1) * S], want[j]), (b, j)
+    erase = [0, k - 1]  # m - 2 Verify rows
+    dec = Plan(k, m, S, batch, ptrs, present=[i not in erase for i in range(n)])
+    dec.tune(reps=1)
+    for b in range(batch):
+        for i in erase:
+            s0 = off + (b * n + i) * S
+            buf[s0:s0 + S].zero_()
+    dec.launch()
+    assert not dec.corrupt()
+    assert np.array_equal(buf.cpu().numpy()[off:off + total], host)

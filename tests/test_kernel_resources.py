@@ -65,7 +65,7 @@ def test_lds_kernel_occupancy(kernels):
     (16-byte entries): 4 waves."""
     for k in _lds(kernels):
         r = int(re.search(r"rs_apply_lds<(\d+),", k["name"]).group(1))
-        realign = _policy(k)[10] == "true"
+        realign = _policy(k)[10] not in ("false", "0")
         want = 8 if r <= 4 else (6 if realign else 7) if r <= 8 else 4
         assert k["waves_per_simd"] >= want, (k["name"], k["vgprs"], k["waves_per_simd"])
         if r > 8:

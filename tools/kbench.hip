@@ -253,6 +253,8 @@ int main(int argc, char** argv) {
     a.stripe_stride = B > 1 ? static_cast<uint64_t>(pitch) * n : 0;
     a.in_misalign = 0;
     for (const uint8_t* p : in) a.in_misalign |= static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u;
+    a.out_misalign = 0;
+    for (uint8_t* p : out) a.out_misalign |= static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u;
   }
 
   using namespace dev;
@@ -486,6 +488,11 @@ int main(int argc, char** argv) {
     vs.push_back(Variant{"probe 63-vec waves", [m](const ApplyArgs& a, hipStream_t s) { p1[m - 1](a, s); }, false});
     vs.push_back(Variant{"probe 64-vec waves lane63 idle", [m](const ApplyArgs& a, hipStream_t s) { p2[m - 1](a, s); }, false});
     vs.push_back(Variant{"realign consec", [m](const ApplyArgs& a, hipStream_t s) { rc[m - 1](a, s); }});
+    static void (*const ro[8])(const ApplyArgs&, hipStream_t) = {
+#define KB_P(R) [](const ApplyArgs& a, hipStream_t s) { ApplyArgs b = a; b.tail_in_vec = 1; launch_lds<R, Policy<(R <= 4 ? 8 : 2), 1, true, true, false, 512, 2, 0, 0, false, 2>>(b, s); }
+        KB_P(1), KB_P(2), KB_P(3), KB_P(4), KB_P(5), KB_P(6), KB_P(7), KB_P(8)};
+#undef KB_P
+    vs.push_back(Variant{"realign out (loads+stores)", [m](const ApplyArgs& a, hipStream_t s) { ro[m - 1](a, s); }});
     vs.push_back(Variant{"plain consec", [m](const ApplyArgs& a, hipStream_t s) {
                            if (m == 4) launch_lds<4, Policy<2, 1, true, true, false, 512, 2, 0>>(a, s);
                            else if (m == 8) launch_lds<8, Policy<2, 1, true, true, false, 512, 2, 0>>(a, s);

@@ -4,7 +4,7 @@
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; TAG="${1:-wtp}"
 OUT="$R/gpurun_out/$TAG"; mkdir -p "$OUT"
-export KB_PROBE63=1 KB_KEEP="probe 6|realign consec|plain consec|nomath consec"
+export KB_PROBE63=1 KB_KEEP="probe 6|realign consec|realign out|plain consec|nomath consec"
 run() {  # name k m S B palign
   timeout -k 10 200 "$R/tools/kbench" $2 $3 $4 $5 7 10 $6 > "$OUT/$1.log" 2>&1 || exit $?
   grep -vE "^RS|variant" "$OUT/$1.log" | sed "s/^/$1 /"
