@@ -6,9 +6,11 @@
 // Two kernels (DESIGN.md "Kernels"); launch_apply in rs_kernels.hip picks one per launch:
 //  * rs_apply_lds — every launch with k >= 4 inputs or R >= 5 rows (the bench's kernel).
 //    Per data byte, two LDS lookups into per-shard nibble tables return the products for
-//    all R rows at once. Table addresses are formed by v_perm_b32, and partial products
-//    are combined by v_bitop3 as a three-input XOR. The tables are staged into LDS once
-//    per block.
+//    all R rows at once. Table addresses are formed by v_perm_b32 (R <= 8) or
+//    v_or_b32_sdwa (R 9..16: no VGPR for the table base, 4 waves per SIMD), and partial
+//    products are combined by v_bitop3 as a three-input XOR. The tables are staged into
+//    LDS once per block. Misaligned shards (upstream Split layout at odd S) take its
+//    REALIGN form: aligned loads and stores, realigned in registers by DPP + v_alignbyte.
 //  * rs_apply_vec — k <= 3 with R <= 4. GF multiply by a wave-uniform coefficient c on 4
 //    packed bytes = three v_perm_b32 byte-selects from 8-byte tables:
 //    c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6] (gf256.hpp perm_tables). The tables arrive
@@ -17,8 +19,9 @@
 // global_load_dwordx4 (non-temporal), keep the R outputs in registers and write (or,
 // for Verify rows, compare) them once: (K + R) * 16 bytes of compulsory HBM traffic per
 // vector, nothing re-read (rocprofv3 FETCH/WRITE_SIZE = algorithmic bytes).
-// Ragged tails (S % 16) take the byte kernel. Shard pointers need no alignment: 16-B
-// global accesses at any byte address are legal on gfx950 (rs_kernels.hpp).
+// Ragged tails (S % 16) are computed by each stripe's first tile, one byte per thread
+// (the byte kernel rs_apply_bytes remains for S < 16). Shard pointers need no alignment:
+// 16-B global accesses at any byte address are legal on gfx950 (rs_kernels.hpp).
 #pragma once
 
 #include <algorithm>
