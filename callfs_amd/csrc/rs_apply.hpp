@@ -312,7 +312,7 @@ void rs_apply_vec(ApplyArgs a) {
         if (!live[u]) continue;
         const uint4 o = make_uint4(acc[u][r][0], acc[u][r][1], acc[u][r][2], acc[u][r][3]);
         if (cmp) {
-          const uint4 y = dst[u * BS];
+          const uint4 y = load16<P>(dst + u * BS);  // non-temporal, as in rs_apply_lds
           bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) != 0;
         } else {
           store16<P>(dst + u * BS, o);
@@ -758,7 +758,9 @@ void rs_apply_lds(ApplyArgs a) {
       }
       if (P::REALIGN && !active) continue;
       if ((a.verify_mask >> r) & 1u) {
-        const uint4 y = *dst;
+        // non-temporal like the input loads: the all-Verify decode (every download,
+        // codec.go:59) ran 76.3-77.9 -> 79.7-80.2 % with them (tools/verify_nt_probe.sh)
+        const uint4 y = load16<P>(dst);
         bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) != 0;
       } else {
         store16<P>(dst, o);
