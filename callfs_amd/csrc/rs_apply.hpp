@@ -35,6 +35,8 @@ namespace dev {
 
 constexpr int kBlock = 256;
 
+
+
 template <class T>
 using cptr = const __attribute__((address_space(4))) T*;
 
@@ -100,8 +102,12 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //            global_load_dwordx4
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
           int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, int REALIGN_ = 0,
-          bool SDWA_ = false, int PROBE_ = 0>
+          bool SDWA_ = false, int PROBE_ = 0, int VPF_ = 0>
 struct Policy {
+  // > 0: Verify rows' stored vectors are loaded VPF shards before the end of the input
+  // loop instead of after it (R <= 4, plain loads, ring of three only)
+  static constexpr int VPF = VPF_;
+  static_assert(VPF_ == 0 || (REALIGN_ == 0 && RING_ == 0), "VPF: plain ring-of-three kernel only");
   // tools/kbench layout probes (never dispatched): 1 = 63-vector waves (the REALIGN
   // tiling) with plain loads, lane 63 idle; 2 = 64-vector waves, lane 63 idle
   static constexpr int PROBE = PROBE_;
@@ -685,6 +691,14 @@ void rs_apply_lds(ApplyArgs a) {
     for (int w = 0; w < 4; ++w)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[w][j] = lds_zero<RT>();
+    // Verify rows' stored vectors, loaded VPF shards before the end of the input loop:
+    // a compare load issued after the loop leaves each wave a full memory latency with
+    // nothing to do (tools/verify_prefetch_probe.sh: one write + three compare rows 71.6
+    // -> 74.1 %, four compare rows 78.0 -> 80.9 %)
+    constexpr bool kVpf = P::VPF > 0 && RT <= 4;
+    uint4 vpre[kVpf ? RT : 1];
+#pragma unroll
+    for (int r = 0; r < (kVpf ? RT : 1); ++r) vpre[r] = make_uint4(0, 0, 0, 0);
 
     if constexpr (P::REALIGN) {
       static_assert(!P::NOMATH, "REALIGN: no NOMATH form");
@@ -704,6 +718,14 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll 1
       for (int i = 0; i < K; ++i) {
         if (i + 2 < K) x2 = ld(i + 2);
+        if constexpr (kVpf) {
+          if (i == (K > P::VPF ? K - P::VPF : 0)) {
+#pragma unroll
+            for (int r = 0; r < RT; ++r)
+              if (r < R && ((a.verify_mask >> r) & 1u))
+                vpre[r] = load16<P>(reinterpret_cast<const uint4*>(out[r]) + v0);
+          }
+        }
         if constexpr (P::NOMATH) {
 #pragma unroll
           for (int w = 0; w < 4; ++w) acc[w][0] = acc[w][0] ^ lds_splat<RT>(word(x0, w));
@@ -760,7 +782,9 @@ void rs_apply_lds(ApplyArgs a) {
       if ((a.verify_mask >> r) & 1u) {
         // non-temporal like the input loads: the all-Verify decode (every download,
         // codec.go:59) ran 76.3-77.9 -> 79.7-80.2 % with them (tools/verify_nt_probe.sh)
-        const uint4 y = load16<P>(dst);
+        uint4 y;
+        if constexpr (kVpf) y = vpre[r];
+        else y = load16<P>(dst);
         bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) != 0;
       } else {
         store16<P>(dst, o);

@@ -56,6 +56,15 @@ using LdsG8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 2>;
 using LdsG2Policy = dev::Policy<2, 1, true, true, false, 512, 2, 5>;
 using LdsQ8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 6>;
 using LdsQ16Policy = dev::Policy<2, 1, true, true, false, 512, 2, 8>;
+// Launch groups of R <= 4 rows with Verify rows load the compared vectors 4 shards before
+// the end of the input loop (rs_apply.hpp Policy::VPF): tools/verify_prefetch_probe.sh,
+// profiles/r02/verify_prefetch/, RS(10,4) 1 MiB x 256, % of 8 TB/s, after the loop ->
+// prefetch distance 2 / 4 / 6 / 8: one write + three compare rows 71.6 -> 72.7 / 74.1 /
+// 73.7 / 73.3, four compare rows 78.0 -> 79.3 / 80.9 / 80.8 / 79.5. Without Verify rows
+// the same code measured 0.4 points slower (the extra registers), so encode launches keep
+// the policies above: one instance per tile order.
+template <int ORD>
+using LdsVerifyPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 4>;
 // Misaligned shards (upstream Split layout of contiguous objects at odd S) with R <= 8:
 // loads from aligned addresses realigned in registers, and parity stores to aligned
 // addresses realigned the same way (62 vectors per wave; the bytes no aligned block
@@ -174,6 +183,13 @@ const auto kLdsG8 = lds_order_table<LdsG8Policy>(std::make_integer_sequence<int,
 const auto kLdsG2 = lds_order_table<LdsG2Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ8 = lds_order_table<LdsQ8Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ16 = lds_order_table<LdsQ16Policy>(std::make_integer_sequence<int, 8>{});
+// [tile order][R - 1] for R <= 4 with Verify rows (TileOrder values index the first level)
+const std::array<std::array<VecFn, 4>, 5> kLdsVerify = {
+    lds_order_table<LdsVerifyPolicy<0>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsVerifyPolicy<2>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsVerifyPolicy<5>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsVerifyPolicy<6>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsVerifyPolicy<8>>(std::make_integer_sequence<int, 4>{})};
 template <int... Rs>
 constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1>>...};
@@ -289,13 +305,18 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
-          switch (order >= 0 && order != kOrderRealign ? static_cast<TileOrder>(order) : lds_rule(a)) {
+          const TileOrder ord =
+              order >= 0 && order != kOrderRealign ? static_cast<TileOrder>(order) : lds_rule(a);
+          switch (ord) {
             case TileOrder::kGroup8: fn = kLdsG8[a.R - 1]; break;
             case TileOrder::kGroup2: fn = kLdsG2[a.R - 1]; break;
             case TileOrder::kSeg8: fn = kLdsQ8[a.R - 1]; break;
             case TileOrder::kSeg16: fn = kLdsQ16[a.R - 1]; break;
             case TileOrder::kConsecutive: break;
           }
+          const uint32_t rows = (1u << a.R) - 1;
+          const int oi = static_cast<int>(ord);
+          if (a.R <= 4 && (a.verify_mask & rows) && oi >= 0 && oi < 5) fn = kLdsVerify[oi][a.R - 1];
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }
@@ -312,6 +333,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
                           LdsG8Policy::BS == LdsPolicy::BS && LdsG2Policy::BS == LdsPolicy::BS &&
                           LdsQ8Policy::BS == LdsPolicy::BS && LdsQ16Policy::BS == LdsPolicy::BS &&
                           LdsWideQ8Policy::BS == LdsPolicy::BS &&
+                          LdsVerifyPolicy<0>::TILE_VECS == LdsPolicy::TILE_VECS &&
                           LdsRealignOutPolicy::BS == LdsPolicy::BS &&
                           LdsRealignOut8Policy::TILE_VECS == LdsRealignOutPolicy::TILE_VECS,
                       "one grid shape for every LDS policy");
