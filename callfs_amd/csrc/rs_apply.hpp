@@ -185,13 +185,15 @@ __device__ __forceinline__ void mac_one(uint32_t (&acc)[U][RT][4], const uint4 (
 // kernel (one byte per thread): odd-S launches need no second kernel. The first tile, not
 // the last: the tail is a chain of K byte loads, and in the stripe's last tile (the
 // grid's last for the last stripe) it outlasted the other waves and delayed the kernel's
-// end by ~2 %. Loads are issued kTailLoads at a time.
-constexpr int kTailLoads = 4;
+// end by ~2 %. Loads are issued tail_loads<RT>() at a time: 8 where the
+// kernel has registers to spare (R <= 4), 4 otherwise (8 took R = 8 from 68 to 73 VGPRs).
+template <int RT>
+constexpr int tail_loads() { return RT <= 4 ? 8 : 4; }
 template <int RT>
 __device__ __forceinline__ void tail_bytes(cptr<const uint8_t*> in, uint64_t b, int i0, int K,
-                                           uint32_t (&x)[kTailLoads]) {
+                                           uint32_t (&x)[tail_loads<RT>()]) {
 #pragma unroll
-  for (int j = 0; j < kTailLoads; ++j) x[j] = i0 + j < K ? in[i0 + j][b] : 0u;
+  for (int j = 0; j < tail_loads<RT>(); ++j) x[j] = i0 + j < K ? in[i0 + j][b] : 0u;
 }
 template <int RT>
 __device__ __forceinline__ void vec_tail(const ApplyArgs& a, cptr<const uint8_t*> in,
@@ -203,10 +205,10 @@ __device__ __forceinline__ void vec_tail(const ApplyArgs& a, cptr<const uint8_t*
   uint32_t acc[RT];
 #pragma unroll
   for (int r = 0; r < RT; ++r) acc[r] = 0;
-  for (int i0 = 0; i0 < a.K; i0 += kTailLoads) {
-    uint32_t x[kTailLoads];
+  for (int i0 = 0; i0 < a.K; i0 += tail_loads<RT>()) {
+    uint32_t x[tail_loads<RT>()];
     tail_bytes<RT>(in, b, i0, a.K, x);
-    for (int j = 0; j < kTailLoads && i0 + j < a.K; ++j) {
+    for (int j = 0; j < tail_loads<RT>() && i0 + j < a.K; ++j) {
       const Sel sel = selectors(x[j]);
       const cptr<uint32_t> t = tabs + static_cast<size_t>(i0 + j) * RT * 5;
 #pragma unroll
@@ -581,10 +583,10 @@ __device__ __forceinline__ void lds_tail(const ApplyArgs& a, cptr<const uint8_t*
   if (threadIdx.x >= nt) return;
   const uint64_t b = a.nvec * 16 + threadIdx.x;
   typename LdsAcc<RT>::T t = lds_zero<RT>();
-  for (int i0 = 0; i0 < a.K; i0 += kTailLoads) {
-    uint32_t x[kTailLoads];
+  for (int i0 = 0; i0 < a.K; i0 += tail_loads<RT>()) {
+    uint32_t x[tail_loads<RT>()];
     tail_bytes<RT>(in, b, i0, a.K, x);
-    for (int j = 0; j < kTailLoads && i0 + j < a.K; ++j) {
+    for (int j = 0; j < tail_loads<RT>() && i0 + j < a.K; ++j) {
       const uint32_t base = lds0 + static_cast<uint32_t>(i0 + j) * 32u * W;
       t = t ^ lds_lookup<RT>(base + (x[j] & 15u) * W) ^
           lds_lookup<RT>(base + 16u * W + (x[j] >> 4) * W);
@@ -612,10 +614,10 @@ __device__ __forceinline__ void lds_edges(const ApplyArgs& a, cptr<const uint8_t
   if (!head && b >= a.S) return;
   if (head && b >= a.S) return;
   typename LdsAcc<RT>::T t = lds_zero<RT>();
-  for (int i0 = 0; i0 < a.K; i0 += kTailLoads) {
-    uint32_t x[kTailLoads];
+  for (int i0 = 0; i0 < a.K; i0 += tail_loads<RT>()) {
+    uint32_t x[tail_loads<RT>()];
     tail_bytes<RT>(in, b, i0, a.K, x);
-    for (int jj = 0; jj < kTailLoads && i0 + jj < a.K; ++jj) {
+    for (int jj = 0; jj < tail_loads<RT>() && i0 + jj < a.K; ++jj) {
       const uint32_t base = lds0 + static_cast<uint32_t>(i0 + jj) * 32u * W;
       t = t ^ lds_lookup<RT>(base + (x[jj] & 15u) * W) ^
           lds_lookup<RT>(base + 16u * W + (x[jj] >> 4) * W);

@@ -166,7 +166,7 @@ void rs_plan_destroy(rs_plan* plan);
  * by 1-2 %. rs_plan_tune times each launch group of the plan in every
  * tile order its kernel offers (`reps` launches per order, three rounds) and keeps the
  * fastest for later rs_plan_launch calls; the measured rule's order stays unless another
- * is > 0.3 % faster. Synchronous on `stream`; RS_E_ARG while `stream` is capturing. The
+ * is > 1 % faster. Synchronous on `stream`; RS_E_ARG while `stream` is capturing. The
  * tuning launches recompute the plan's outputs from its inputs (same bytes; Verify rows
  * may flag status exactly as rs_plan_launch would). orders (NULL when max_groups == 0):
  * the chosen order per launch group, up to max_groups entries (RS_ORDER_* or -1 = the
