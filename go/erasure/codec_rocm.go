@@ -307,10 +307,15 @@ func (c *Codec) RepairBatch(objs [][][]byte, profile ErasureProfile) []error {
 	}
 	rc := C.rs_reconstruct_batch(gpuCtx, C.int(k), C.int(m), C.int(len(objs)), ptrs.at(0),
 		&lens[0], 1, &status[0])
-	switch rc {
-	case C.RS_OK, C.RS_E_CORRUPT, C.RS_E_TOO_FEW_SHARDS, C.RS_E_SHARD_SIZE, C.RS_E_NO_DATA, C.RS_E_ARG:
+	stripeArg := false // RS_E_ARG is per-stripe only when some stripe reports it
+	for _, st := range status {
+		stripeArg = stripeArg || st == C.RS_E_ARG
+	}
+	switch {
+	case rc == C.RS_OK, rc == C.RS_E_CORRUPT, rc == C.RS_E_TOO_FEW_SHARDS,
+		rc == C.RS_E_SHARD_SIZE, rc == C.RS_E_NO_DATA, rc == C.RS_E_ARG && stripeArg:
 		// per-stripe statuses are valid (RS_E_ARG: a stripe with a nil present entry)
-	default:
+	default: // a call-level error: no status was written
 		for b := range errs {
 			if errs[b] == nil {
 				errs[b] = decodeErr(rc)

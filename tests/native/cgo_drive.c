@@ -137,6 +137,30 @@ static void argument_paths(rs_ctx* ctx, int k, int m, size_t S, uint8_t* const* 
     free_call(&c);
     free(ln);
   }
+  /* RepairBatch (rs_reconstruct_batch): per-stripe statuses vs call-level RS_E_ARG. Stripe 0
+     lacks m+1 shards, stripe 1 has a present entry with a nil pointer; neither touches the
+     device, lens stays as it was, and a call-level error writes no status at all. */
+  {
+    uint8_t** bp = (uint8_t**)malloc(sizeof(uint8_t*) * 2 * (size_t)n);
+    size_t* bl = (size_t*)malloc(sizeof(size_t) * 2 * (size_t)n);
+    for (int i = 0; i < n; i++) {
+      const int gone = i >= n - (m + 1);
+      bp[i] = gone ? NULL : shards[i];
+      bl[i] = gone ? 0 : S;
+      bp[n + i] = i == n - 1 ? NULL : shards[i];
+      bl[n + i] = S;
+    }
+    int st[2] = {-12345, -12345};
+    CHECK(rs_reconstruct_batch(ctx, k, m, 2, bp, bl, 1, st) == RS_E_TOO_FEW_SHARDS);
+    CHECK(st[0] == RS_E_TOO_FEW_SHARDS && st[1] == RS_E_ARG);
+    for (int i = 0; i < n; i++) CHECK(bl[i] == (i >= n - (m + 1) ? 0 : S) && bl[n + i] == S);
+    st[0] = st[1] = -12345;
+    CHECK(rs_reconstruct_batch(ctx, k, m, 2, bp, bl, 1, NULL) == RS_E_ARG);
+    CHECK(rs_reconstruct_batch(NULL, k, m, 2, bp, bl, 1, st) == RS_E_ARG);
+    CHECK(st[0] == -12345 && st[1] == -12345); /* the shim tells call-level from per-stripe so */
+    free(bl);
+    free(bp);
+  }
   /* encode: empty object (Split -> ErrShortData), also for a k+m > 256 profile */
   {
     size_t ss = 7;
