@@ -277,6 +277,39 @@ def test_plan_encode_matches_oracle(native_lib, k, m, S, batch):
     assert plan.bytes == batch * S * (k + m)
 
 
+@pytest.mark.parametrize("fill", [0x00, 0xFF])
+@pytest.mark.parametrize("k,m,S,batch", [(10, 4, (1 << 20) + 5, 3), (3, 2, 349_526, 2),
+                                         (10, 12, 65_541, 2), (20, 8, 4099, 3)])
+def test_plan_constant_inputs(native_lib, fill, k, m, S, batch):
+    """SURVEY §8(d) sanity inputs: all-zero data encodes to all-zero parity; all-0xFF data
+    gives parity row j = 0xFF * XOR_i P[j][i] in every byte (each kernel family: v_perm for
+    k <= 3, LDS for R <= 8 and 9..16, ragged tails); then a decode with m erasures from
+    the constant shards restores them, and Verify passes."""
+    import torch
+    from callfs_amd.device import Plan, StripeBatch
+    sb = StripeBatch(k, m, S, batch, torch.device("cuda:0"))
+    sb.buf.fill_(fill)
+    sb.buf[:, k:].fill_(0x5A)  # parity rows start as garbage
+    Plan.for_batch(sb).launch()
+    torch.cuda.synchronize()
+    host = sb.buf[:, :, :S].cpu().numpy()
+    col = [np.full(1, fill, np.uint8) for _ in range(k)]
+    want = cref.encode(col, k, m)
+    for j in range(m):
+        assert (host[:, k + j] == want[j][0]).all(), j
+    if fill == 0:
+        assert not host[:, k:].any()
+    ref = sb.buf.clone()
+    erase = list(range(0, k + m, max(1, (k + m) // m)))[:m]
+    for i in erase:
+        sb.buf[:, i].fill_(0x33)
+    present = [i not in erase for i in range(k + m)]
+    dec = Plan.for_batch(sb, present=present)
+    dec.launch()
+    assert not dec.corrupt()
+    assert torch.equal(sb.buf[:, :, :S], ref[:, :, :S])
+
+
 @pytest.mark.parametrize("erase", ERASURES_10_4)
 def test_plan_decode_restores_and_verifies(native_lib, erase):
     import torch
