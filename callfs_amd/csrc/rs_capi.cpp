@@ -1374,6 +1374,8 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
 // left the rule for an order that then timed 0.5-1 % slower: tools/tune_small.sh).
 namespace {
 constexpr int kTuneRounds = 3;
+constexpr float kTuneWarmMs = 150.0f;
+constexpr int kTuneWarmBatches = 400;
 // CALLFS_RS_TUNE_LOG=1: rs_plan_tune prints each candidate's time per launch to stderr
 bool tune_log() {
   static const bool on = [] {
@@ -1407,10 +1409,23 @@ int rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_gro
     const std::vector<int> cand = order_candidates(a);
     if (cand.size() < 2) continue;
     std::vector<float> best(cand.size(), 1e30f);
-    // warm-up in the rule's order first: the first candidate timed right after other
-    // work (the bench's round-trip check) measured up to 3 % slow
-    for (int r = 0; r < reps && rc == RS_OK; ++r)
-      if (launch_apply(a, s, false, cand[0]) != hipSuccess) rc = RS_E_HIP;
+    // warm-up in the rule's order first, by time: a chip that has just come out of other
+    // (or no) work runs the bench shape up to 4 % slow for ~100 ms (bench.py at 5 vs 100
+    // warm-up steps, profiles/r02/warmup/), and candidates timed during that ramp favour
+    // whichever is timed last. Batches of `reps` launches until kTuneWarmMs of device
+    // time have passed (at most kTuneWarmBatches batches).
+    {
+      float warm = 0;
+      for (int b = 0; b < kTuneWarmBatches && warm < kTuneWarmMs && rc == RS_OK; ++b) {
+        bool ok = hipEventRecord(e0, s) == hipSuccess;
+        for (int r = 0; r < reps && ok; ++r) ok = launch_apply(a, s, false, cand[0]) == hipSuccess;
+        float ms = 0;
+        ok = ok && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+             hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+        if (!ok) rc = RS_E_HIP;
+        warm += ms;
+      }
+    }
     for (int round = 0; round < kTuneRounds && rc == RS_OK; ++round) {
       for (size_t j = 0; j < cand.size() && rc == RS_OK; ++j) {
         const size_t c = (j + round) % cand.size();

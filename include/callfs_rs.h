@@ -163,7 +163,8 @@ void rs_plan_destroy(rs_plan* plan);
 
 /* Tile-order tuning (no upstream counterpart; an autotuner for repeated launches).
  * Which order of column tiles HBM serves best for a shape varies between MI355X boxes
- * by 1-2 %. rs_plan_tune times each launch group of the plan in every
+ * by 1-2 %. rs_plan_tune warms the device up in the rule's order (~150 ms
+ * of launches), then times each launch group of the plan in every
  * tile order its kernel offers (`reps` launches per order, three rounds) and keeps the
  * fastest for later rs_plan_launch calls; the measured rule's order stays unless another
  * is > 1 % faster. Synchronous on `stream`; RS_E_ARG while `stream` is capturing. The
