@@ -1376,6 +1376,20 @@ namespace {
 constexpr int kTuneRounds = 3;
 constexpr float kTuneWarmMs = 150.0f;
 constexpr int kTuneWarmBatches = 400;
+// CALLFS_RS_TUNE_BAR=<percent>: how much faster than the rule's order another order must
+// time to replace it (default 1)
+float tune_bar() {
+  static const float v = [] {
+    const char* e = std::getenv("CALLFS_RS_TUNE_BAR");
+    if (e && *e) {
+      const float x = std::strtof(e, nullptr);
+      if (x >= 0.0f && x < 50.0f) return x;
+    }
+    return 1.0f;
+  }();
+  return v;
+}
+
 // CALLFS_RS_TUNE_LOG=1: rs_plan_tune prints each candidate's time per launch to stderr
 bool tune_log() {
   static const bool on = [] {
@@ -1445,7 +1459,7 @@ int rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_gro
     if (rc != RS_OK) break;
     size_t win = 0;  // cand[0] is the rule's order
     for (size_t c = 1; c < cand.size(); ++c)
-      if (best[c] < best[win] * (win == 0 ? 0.99f : 1.0f)) win = c;
+      if (best[c] < best[win] * (win == 0 ? 1.0f - tune_bar() / 100.0f : 1.0f)) win = c;
     chosen[gi] = cand[win];
     if (tune_log()) {
       std::fprintf(stderr, "rs_plan_tune: group %zu (K=%d R=%d S=%zu batch=%d):", gi, a.K, a.R,
