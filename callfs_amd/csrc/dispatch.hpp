@@ -9,8 +9,11 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
+#include <mutex>
 #include <vector>
 
 namespace callfs {
@@ -43,6 +46,59 @@ inline int split_ways(size_t ndev, int lanes_per_device, size_t S, int n, int ba
   long ways = ways_req > 0 ? ways_req : static_cast<long>(ndev);
   ways = std::max(1L, std::min(ways, static_cast<long>(ndev) * lanes_per_device));
   return static_cast<int>(std::max<size_t>(1, std::min<size_t>(static_cast<size_t>(ways), S >> 22)));
+}
+
+// ways_req for split_ways from CALLFS_RS_SPLIT_WAYS: unset (nullptr) = one way per
+// device; an explicit value <= 1 (0, negative, not a number) keeps every object on one
+// device, which is what 0 meant before the per-device default existed.
+inline int split_ways_request(const char* env) {
+  if (!env) return 0;
+  const long v = std::strtol(env, nullptr, 10);
+  return v > 1 ? static_cast<int>(std::min(v, 1L << 20)) : 1;
+}
+
+// One-time setup per (device, key), e.g. the > 64 KiB dynamic-LDS opt-in of the wide
+// kernels: hipFuncSetAttribute applies to the calling thread's current device only, so
+// a once-flag per kernel would leave every device but the first without it. `run`
+// calls f() the first time a (device, key) pair is seen and returns whether it did;
+// concurrent callers of one pair wait until f() has returned. Devices outside
+// [0, kMaxDevices) and keys outside [0, 64) run f() every time.
+class DeviceOnce {
+ public:
+  template <class F>
+  bool run(int device, int key, F&& f) {
+    if (device < 0 || device >= kMaxDevices || key < 0 || key >= 64) {
+      f();
+      return true;
+    }
+    const uint64_t bit = 1ull << key;
+    if (done_[device].load(std::memory_order_acquire) & bit) return false;
+    std::lock_guard<std::mutex> g(mu_);
+    if (done_[device].load(std::memory_order_relaxed) & bit) return false;
+    f();
+    done_[device].fetch_or(bit, std::memory_order_release);
+    return true;
+  }
+  bool done(int device, int key) const {
+    return device >= 0 && device < kMaxDevices && key >= 0 && key < 64 &&
+           (done_[device].load(std::memory_order_acquire) >> key) & 1u;
+  }
+
+ private:
+  std::atomic<uint64_t> done_[kMaxDevices] = {};
+  std::mutex mu_;
+};
+
+// rs_init: per-device setup of every selected device (make it current, then run `setup`
+// for each key); returns false at the first device that cannot be made current.
+template <class SetDevice, class Setup>
+bool setup_devices(const std::vector<int>& devs, DeviceOnce& once, int nkeys,
+                   SetDevice&& set_device, Setup&& setup) {
+  for (int d : devs) {
+    if (!set_device(d)) return false;
+    for (int key = 0; key < nkeys; ++key) once.run(d, key, [&] { setup(d, key); });
+  }
+  return true;
 }
 
 // Column boundaries c[0..ways] of an S-byte shard: c[0] = 0, c[ways] = S, interior

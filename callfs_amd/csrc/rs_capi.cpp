@@ -422,7 +422,8 @@ class PinnedRegistry {
 // after the call ran 25-30x slower than one that reuses buffers (RS(4,2) 256 MiB,
 // zero-copy: 1.6 vs 48 GiB/s encode). rs_host_free parks a buffer here;
 // rs_host_alloc takes the smallest parked buffer that fits without wasting more than a
-// quarter of it. Parked bytes are capped by CALLFS_RS_HOST_POOL_BYTES (default 8 GiB;
+// quarter of it, both sides counted in 2 MiB granules. Parked bytes are capped by
+// CALLFS_RS_HOST_POOL_BYTES (default 4 GiB;
 // 0 disables parking): beyond it the largest parked buffers are released.
 class HostPool {
  public:
@@ -432,9 +433,12 @@ class HostPool {
   };
   // a parked buffer of at least n bytes, or {nullptr, 0}
   Buf take(size_t n) {
+    // compare in allocation granules: a 4 KiB or 1 MiB request was allocated as one
+    // 2 MiB granule, and that buffer must serve the next request of the same size
+    const size_t want = granule(n);
     std::lock_guard<std::mutex> g(mu_);
-    auto it = idle_.lower_bound(n);
-    if (it == idle_.end() || it->first - n > it->first / 4) return {nullptr, 0};
+    auto it = idle_.lower_bound(want);
+    if (it == idle_.end() || it->first - want > it->first / 4) return {nullptr, 0};
     Buf b{it->second, it->first};
     idle_bytes_ -= it->first;
     idle_.erase(it);
@@ -470,12 +474,16 @@ class HostPool {
     std::lock_guard<std::mutex> g(mu_);
     return idle_bytes_;
   }
+  // capacity rs_host_alloc gives a fresh buffer of n bytes (2 MiB granules, so buffers
+  // freed by one request fit the next request of similar size)
+  static size_t granule(size_t n) { return (n + kGranule - 1) / kGranule * kGranule; }
+  static constexpr size_t kGranule = 2u << 20;
 
  private:
   static size_t limit() {
     static const size_t v = [] {
       const char* e = std::getenv("CALLFS_RS_HOST_POOL_BYTES");
-      return e ? static_cast<size_t>(std::strtoull(e, nullptr, 0)) : (8ull << 30);
+      return e ? static_cast<size_t>(std::strtoull(e, nullptr, 0)) : (4ull << 30);
     }();
     return v;
   }
@@ -630,7 +638,7 @@ int split_ways(const rs_ctx* ctx, size_t S, int n, int batch) {
   const char* e = std::getenv("CALLFS_RS_SPLIT_MIN_BYTES");
   const unsigned long long min_bytes = e ? std::strtoull(e, nullptr, 0) : (256ull << 20);
   const char* w = std::getenv("CALLFS_RS_SPLIT_WAYS");
-  const int ways_req = w ? std::atoi(w) : 0;
+  const int ways_req = split_ways_request(w);  // unset: one per device; <= 1: no split
   return callfs::split_ways(ctx->devs.size(), kMaxLanesPerDevice, S, n, batch, min_bytes,
                             ways_req);
 }
@@ -998,6 +1006,14 @@ int rs_init(rs_ctx** out, unsigned device_mask) {
     ctx->devs.push_back(std::move(dev));
   }
   if (ctx->devs.empty()) return RS_E_HIP;
+  // the wide kernels' > 64 KiB dynamic-LDS opt-in, on every selected device (it is a
+  // per-device attribute; launch_apply repeats it on first use for other devices)
+  {
+    DeviceGuard dg;
+    std::vector<int> ids;
+    for (auto& d : ctx->devs) ids.push_back(d->id);
+    if (!callfs::prepare_devices(ids)) return RS_E_HIP;
+  }
   *out = ctx.release();
   return RS_OK;
 }
@@ -1014,8 +1030,7 @@ int rs_host_alloc(rs_ctx* ctx, size_t bytes, void** out) {
   *out = nullptr;
   HostPool::Buf b = ctx->host_pool.take(bytes);
   if (!b.p) {
-    // 2 MiB granules: buffers freed by one request fit the next request of similar size
-    b.cap = round_up(bytes, 2u << 20);
+    b.cap = HostPool::granule(bytes);
     // portable: every device of the context may use it. Coherent: the kernels read and
     // write it in place (zero-copy), and the caller refills the same buffer between
     // calls, so device caches must not keep its lines across launches.
@@ -1504,6 +1519,10 @@ int rs_plan_status(rs_plan* plan, void* stream, int* corrupt) {
 }
 
 uint64_t rs_plan_bytes(const rs_plan* plan) { return plan ? plan->bytes : 0; }
+
+int rs_plan_groups(const rs_plan* plan) {
+  return plan ? static_cast<int>(plan->tables->groups.size()) : 0;
+}
 
 void rs_plan_destroy(rs_plan* plan) {
   DeviceGuard dg;

@@ -10,6 +10,7 @@
 #include <type_traits>
 #include <utility>
 
+#include "dispatch.hpp"
 #include "rs_apply.hpp"
 #include "tile_order.hpp"
 
@@ -202,7 +203,30 @@ constexpr auto lds_wide_table(std::integer_sequence<int, Rs...>) {
 const auto kLdsWideQ8 = lds_wide_table<LdsWideQ8Policy>(std::make_integer_sequence<int, 8>{});
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
+// Row groups of 9..16 with more than 64 KiB of tables (k > 128) need the dynamic-LDS
+// opt-in, which hipFuncSetAttribute sets for the current device only: one flag per
+// (device, R), key R - 9 (dispatch.hpp DeviceOnce). Both tile-order instances of an R
+// opt in together.
+DeviceOnce g_wide_lds;
+constexpr int kWideKeys = kMaxRowsPerLaunch - 8;
+
+void wide_lds_opt_in(int R) {
+  for (VecFn f : {kLds[R - 1], kLdsWideQ8[R - 9]})
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
+}
+
 }  // namespace
+
+bool prepare_devices(const std::vector<int>& devices) {
+  return setup_devices(
+      devices, g_wide_lds, kWideKeys, [](int d) { return hipSetDevice(d) == hipSuccess; },
+      [](int, int key) { wide_lds_opt_in(key + 9); });
+}
+
+bool wide_lds_ready(int device, int R) {
+  return R >= 9 && R <= kMaxRowsPerLaunch && g_wide_lds.done(device, R - 9);
+}
 
 void set_slice_tiles_for_tuning(long long tiles) {
   g_slice_tiles_override.store(tiles, std::memory_order_relaxed);
@@ -320,14 +344,12 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }
-        if (lds > (64u << 10)) {  // wide groups with many shards: opt in once per kernel
-          // (only R > 8 gets here: both tile-order instances of that R opt in together)
-          static std::once_flag once[kMaxRowsPerLaunch];
-          std::call_once(once[a.R - 1], [&a] {
-            for (VecFn f : {kLds[a.R - 1], kLdsWideQ8[a.R - 9]})
-              (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
-          });
+        if (lds > (64u << 10)) {  // wide groups with many shards (only R > 8 gets here):
+          // the opt-in is per device; rs_init issued it for the context's devices, this
+          // covers plans and device calls on any other device
+          int device = -1;
+          if (hipGetDevice(&device) != hipSuccess) return hipErrorInvalidDevice;
+          g_wide_lds.run(device, a.R - 9, [&a] { wide_lds_opt_in(a.R); });
         }
         static_assert(LdsPolicy::BS == LdsWidePolicy::BS && LdsPolicy::U == LdsWidePolicy::U &&
                           LdsG8Policy::BS == LdsPolicy::BS && LdsG2Policy::BS == LdsPolicy::BS &&

@@ -80,6 +80,13 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false
 // no choice (byte kernel, realigning kernel, S < 16).
 std::vector<int> order_candidates(const ApplyArgs& a);
 
+// rs_init: per-device setup of the kernels for each listed device (the > 64 KiB
+// dynamic-LDS opt-in of the 9..16-row instances, a per-device attribute); leaves the
+// last listed device current. launch_apply also issues it on first use per device.
+bool prepare_devices(const std::vector<int>& devices);
+// whether the opt-in for R rows (9..16) has been issued on `device` (tests)
+bool wide_lds_ready(int device, int R);
+
 // Tuning hook for tools/kbench.hip (not part of the C ABI): tiles per launch slice for
 // every later launch_apply in the process; 0 = never slice, < 0 = the built-in rule
 // (CALLFS_RS_MAX_TILES_PER_LAUNCH or ~4 GiB of traffic per slice).

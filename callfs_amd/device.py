@@ -104,7 +104,7 @@ class Plan:
         and keep the fastest for later launches (synchronous; outputs recomputed to the
         same bytes). Returns the chosen order name per launch group."""
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        n = max(1, -(-self.m // 16))  # launch groups: at most ceil(m / 16) rows of 16
+        n = int(N.lib.rs_plan_groups(self.handle))  # one entry per launch group
         orders = (ctypes.c_int * n)()
         N.check(N.lib.rs_plan_tune(self.handle, ctypes.c_void_p(s.cuda_stream), reps, orders, n),
                 "rs_plan_tune")

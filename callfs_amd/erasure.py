@@ -211,7 +211,10 @@ class Codec:
         out = bytearray(max(int(original_size), 0))
         rc = N.lib.rs_codec_decode(self.context.handle, k, m, ptrs, lens,
                                    _addr(out) if out else None, int(original_size))
-        if rc in (N.RS_OK, N.RS_E_CORRUPT):
+        # upstream Reconstruct (codec.go:55) has filled the nil entries before Verify
+        # (:59) and the join-length check (:73) can fail, so ErrShardCorrupted and
+        # ErrInsufficientShards leave them filled too (as the Go shim does)
+        if rc in (N.RS_OK, N.RS_E_CORRUPT, N.RS_E_INSUFFICIENT):
             for i in range(n):
                 if shards[i] is None or len(shards[i]) == 0:
                     shards[i] = bufs[i]

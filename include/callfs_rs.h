@@ -182,6 +182,9 @@ void rs_plan_destroy(rs_plan* plan);
  * unaligned 16-B accesses in that tile order */
 #define RS_ORDER_REALIGN 32
 int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups);
+/* Launch groups of a plan (the `orders` entries rs_plan_tune can fill): one per up to 16
+ * written or compared rows; 0 for a NULL plan. */
+int  rs_plan_groups(const rs_plan* plan);
 
 /* One-shot device-resident calls (build + launch + free; tables cached per profile).
  * Same pointer layout as rs_plan_create; synchronous on `stream`. rs_decode_dev

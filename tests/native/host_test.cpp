@@ -9,6 +9,10 @@
 //     the launch rules pick the measured orders for known layouts
 //  6. multi-device placement (dispatch.hpp) over mocked device lists: mask selection,
 //     round-robin device slots, split ways and column part boundaries
+//  7. per-device kernel setup (DeviceOnce / setup_devices): the wide kernels' dynamic-LDS
+//     opt-in is issued on every selected device, once per (device, R)
+#include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <random>
 #include <cstring>
@@ -305,6 +309,60 @@ int main() {
       CHECK(w > 0 && w <= S1g / 8 + 4096);
       CHECK(device_slot(0, p, 8) == static_cast<size_t>(p));
     }
+    // CALLFS_RS_SPLIT_WAYS: unset = one per device; explicit <= 1 keeps one device
+    CHECK(split_ways_request(nullptr) == 0);
+    CHECK(split_ways_request("0") == 1 && split_ways_request("-3") == 1);
+    CHECK(split_ways_request("1") == 1 && split_ways_request("x") == 1);
+    CHECK(split_ways_request("5") == 5);
+    CHECK(split_ways(8, 8, S1g, 14, 1, min_b, split_ways_request("0")) == 1);
+    CHECK(split_ways(8, 8, S1g, 14, 1, min_b, split_ways_request(nullptr)) == 8);
+  }
+  // 7. per-device kernel setup (the wide kernels' > 64 KiB dynamic-LDS opt-in is a
+  // per-device attribute): rs_init issues it on every selected device, once per
+  // (device, R); a launch on any device, selected or not, finds it issued or issues it
+  // first; concurrent first launches issue it once
+  {
+    for (unsigned mask : {0u, 0x81u, 0x0Eu}) {
+      DeviceOnce once;
+      const std::vector<int> devs = select_devices(8, mask);
+      int current = -1;
+      std::vector<std::vector<int>> issued(8, std::vector<int>(8, 0));  // [device][R - 9]
+      CHECK(setup_devices(devs, once, 8, [&](int d) { current = d; return true; },
+                          [&](int d, int key) {
+                            CHECK(d == current);  // issued with that device current
+                            issued[d][key]++;
+                          }));
+      for (int d = 0; d < 8; ++d) {
+        const bool sel = std::find(devs.begin(), devs.end(), d) != devs.end();
+        for (int key = 0; key < 8; ++key) {
+          CHECK(issued[d][key] == (sel ? 1 : 0));
+          CHECK(once.done(d, key) == sel);
+        }
+      }
+      // launches on every device in a scrambled order: each (device, R) issued exactly
+      // once overall, before the launch proceeds
+      for (int rep = 0; rep < 3; ++rep)
+        for (int d : {5, 0, 7, 3, 1, 6, 2, 4})
+          for (int key : {7, 0, 3}) {
+            once.run(d, key, [&] { issued[d][key]++; });
+            CHECK(once.done(d, key));
+          }
+      for (int d = 0; d < 8; ++d)
+        for (int key : {7, 0, 3}) CHECK(issued[d][key] == 1);
+    }
+    // a failing set_device stops rs_init
+    DeviceOnce once;
+    CHECK(!setup_devices({0, 1}, once, 8, [](int d) { return d == 0; }, [](int, int) {}));
+    // concurrent first use of one (device, key): one call
+    DeviceOnce once2;
+    std::atomic<int> calls{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < 8; ++t)
+      th.emplace_back([&] {
+        for (int d = 0; d < 8; ++d) once2.run(d, 2, [&] { calls++; });
+      });
+    for (auto& t : th) t.join();
+    CHECK(calls.load() == 8);
   }
   std::printf(fails ? "FAILED %d\n" : "host_test ok\n", fails);
   return fails ? 1 : 0;

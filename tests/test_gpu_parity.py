@@ -199,6 +199,26 @@ def test_decode_error_precedence(codec):
         codec.decode(sh[:5], p, 100)
 
 
+def test_decode_insufficient_fills_missing_entries(codec):
+    """codec.go:55 Reconstruct fills the nil entries before the join-length check at
+    :73 fails, so ErrInsufficientShards leaves them reconstructed (as the Go shim,
+    codec_rocm.go, and upstream do); a Verify failure leaves them filled too."""
+    from callfs_amd import ErasureProfile, ErrInsufficientShards, ErrShardCorrupted
+    p = ErasureProfile(4, 2)
+    data = rnd(11, 1000)
+    full = [bytes(s) for s in codec.encode(data, p)]
+    sh = [None if i in (1, 4) else full[i] for i in range(6)]
+    with pytest.raises(ErrInsufficientShards):
+        codec.decode(sh, p, 4 * len(full[0]) + 1)
+    assert bytes(sh[1]) == full[1] and bytes(sh[4]) == full[4]
+    bad = [bytearray(x) for x in full]
+    bad[5][3] ^= 1
+    sh = [None if i == 0 else bad[i] for i in range(6)]
+    with pytest.raises(ErrShardCorrupted):
+        codec.decode(sh, p, len(data))
+    assert sh[0] is not None and bytes(sh[0]) == full[0]  # rebuilt from shards 1..4
+
+
 def test_encoder_level_reconstruct_verify(native_lib):
     from callfs_amd import encode_shards, reconstruct, verify
     k, m, S = 10, 4, 333_331
@@ -1058,7 +1078,21 @@ def test_host_pool_reuses_freed_buffers(native_lib):
         b = N.PinnedBuffer(k * S - 4096, ctx)  # within a quarter: the parked buffer
         assert b.ptr == pa
         small = N.PinnedBuffer(4096, ctx)
-        assert small.ptr != pa
+        assert small.ptr != pa  # pa is in use
+        # small requests are matched in 2 MiB allocation granules: alloc/free/alloc of
+        # 4 KiB, and then of 1 MiB, gets the same buffer back
+        ps = small.ptr
+        small.close()
+        small = N.PinnedBuffer(4096, ctx)
+        assert small.ptr == ps
+        small.close()
+        mib = N.PinnedBuffer(1 << 20, ctx)
+        assert mib.ptr == ps
+        mib.close()
+        mib = N.PinnedBuffer(1 << 20, ctx)
+        assert mib.ptr == ps
+        mib.close()
+        small = N.PinnedBuffer(4096, ctx)
         par = N.PinnedBuffer(m * S, ctx)
         data = np.frombuffer(rnd(77, k * S), np.uint8)
         b.array[: k * S - 4096] = data[: k * S - 4096]
