@@ -41,6 +41,9 @@ sys.path.insert(0, HERE)
 
 METRIC = "GiB/s device-resident RS encode+decode (k=10,m=4, 1 MiB shards); % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+# host threads per GPU on the driver's boxes: a 1-GPU box grants 16 CPUs though
+# sched_getaffinity / nproc list every CPU of the host
+CPU_SHARE = 16
 
 
 def parse_args(argv=None):
@@ -64,13 +67,15 @@ def parse_args(argv=None):
                    help="bytes of stripes the CPU baseline rotates through (>= 2 GiB: not "
                         "cache-resident)")
     p.add_argument("--cpu-threads", type=int, default=0,
-                   help="CPU baseline threads (0: the visible cores, at most 16 -- the "
-                        "GPU box's CPU share per GPU)")
+                   help="CPU baseline threads (0: the visible cores, at most CPU_SHARE = 16, "
+                        "the GPU box's CPU share per GPU)")
     p.add_argument("--tune", type=int, default=1,
                    help="1: rs_plan_tune each plan before the warmup (times every tile order "
                         "its kernel offers on this box and keeps the fastest; 0: the rule)")
-    p.add_argument("--copy-ceiling", type=int, default=1,
-                   help="1: also time a device copy of the same bytes (roofline.copy_ceiling)")
+    p.add_argument("--ceiling", type=int, default=1,
+                   help="1: also time each plan's traffic ceilings in this process (its read "
+                        "and write streams alone, and the kernel's no-lookup form; "
+                        "roofline.copy_ceiling / roofline.nolookup)")
     p.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
                    help="PMC-measured HBM bytes per launch (rocprofv3 --pmc), if present")
     return p.parse_args(argv)
@@ -145,26 +150,45 @@ def cpu_baseline(sb, k, m, erase, seconds, ws_bytes, threads):
     }
 
 
-def copy_ceiling(total_bytes, dev, stream, reps=10):
-    """GB/s of a device copy moving the same bytes as one encode launch (half read, half
-    written), timed with HIP events on the launch stream; median of `reps`."""
-    n = total_bytes // 2
-    src = torch.empty(n, dtype=torch.uint8, device=dev)
-    dst = torch.empty_like(src)
-    src.fill_(7)
+def _launch_ms(fn, stream, reps=20, warm_ms=30.0):
+    """Mean ms per launch of fn() over `reps` launches, each between two HIP events on
+    `stream`, after >= warm_ms of untimed launches (a kernel timed right after a lighter
+    or heavier one runs off its steady clock for milliseconds)."""
     with torch.cuda.stream(stream):
-        dst.copy_(src)
-        times = []
-        for _ in range(reps):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        while True:
+            for _ in range(4):
+                fn()
+            torch.cuda.synchronize(stream.device)
+            if (time.perf_counter() - t0) * 1e3 >= warm_ms:
+                break
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        for a, b in ev:
             a.record(stream)
-            dst.copy_(src)
+            fn()
             b.record(stream)
-            b.synchronize()
-            times.append(a.elapsed_time(b))
-    times.sort()
-    del src, dst
-    return 2 * n / (times[len(times) // 2] * 1e-3) / 1e9
+        torch.cuda.synchronize(stream.device)
+    return sum(a.elapsed_time(b) for a, b in ev) / reps
+
+
+def plan_ceilings(enc, dec, stream):
+    """Same-process traffic ceilings of the two plans (rs_plan_launch_ceiling, DESIGN.md
+    §6.1): each plan's read streams alone and write streams alone on the production grid
+    and tile order -- their summed time is what the plan's bytes take when reads and writes
+    each run at their own best rate, the achievable denominator -- and the production
+    kernel's no-lookup form. Timed after the bench's timed steps; the plans are relaunched
+    afterwards (decode first, then encode) so every shard holds its true bytes again."""
+    out = {}
+    for name, plan in (("decode", dec), ("encode", enc)):
+        ms = {mode: _launch_ms(lambda: plan.launch_ceiling(mode, stream), stream)
+              for mode in ("read", "write", "nolookup")}
+        plan.corrupt(stream)  # the no-lookup form's Verify rows compare junk: clear
+        plan.launch(stream)
+        if plan.corrupt(stream):
+            raise SystemExit(f"{name} plan relaunched after its ceilings flagged corruption")
+        out[name] = ms
+    return out
 
 
 def load_traffic(path, cfg):
@@ -178,6 +202,31 @@ def load_traffic(path, cfg):
         return None, None, None
     return (t.get("encode_bytes_per_launch"), t.get("decode_bytes_per_launch"),
             os.path.relpath(path, HERE))
+
+
+def ceiling_entry(ceil, name, nbytes, achieved):
+    """roofline.copy_ceiling: the plan's bytes over (read-streams-alone time +
+    write-streams-alone time), both measured live on the same grid and order."""
+    if not ceil:
+        return None
+    ms = ceil[name]
+    gbs = nbytes / ((ms["read"] + ms["write"]) * 1e-3) / 1e9
+    return {"kernel": ("rs_stream_read + rs_stream_write: the launch's read streams alone, "
+                       "then its write streams alone (same grid, tile order, nt 16-B "
+                       "accesses); bytes / summed time"),
+            "achieved": round(gbs, 1), "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4),
+            "frac": round(achieved / gbs, 4),
+            "read_ms": round(ms["read"], 4), "write_ms": round(ms["write"], 4)}
+
+
+def nolookup_entry(ceil, name, nbytes, achieved):
+    """The production kernel's no-lookup form (same loads, stores, grid, order)."""
+    if not ceil:
+        return None
+    gbs = nbytes / (ceil[name]["nolookup"] * 1e-3) / 1e9
+    return {"kernel": "rs_apply_lds NOMATH form (lookups replaced by one XOR per dword)",
+            "achieved": round(gbs, 1), "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4),
+            "frac": round(achieved / gbs, 4), "ms": round(ceil[name]["nolookup"], 4)}
 
 
 def main(argv=None):
@@ -259,8 +308,6 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     barrier()
     torch.cuda.synchronize(dev)
-    if dec.corrupt(stream):
-        raise SystemExit("verify flagged corruption during the timed run")
 
     el = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
@@ -274,7 +321,9 @@ def main(argv=None):
     user_step = 2 * B * k * (S_obj if S_obj else S * world)
     value = args.steps * user_step / elapsed / 2**30
 
-    copy_gbs = copy_ceiling(enc.bytes, dev, stream) if args.copy_ceiling else None
+    if dec.corrupt(stream):
+        raise SystemExit("verify flagged corruption during the timed run")
+    ceil = plan_ceilings(enc, dec, stream) if args.ceiling else None
     cfg = {"k": k, "m": m, "shard_bytes": S, "stripes": B}
     traffic, dec_traffic, tsrc = load_traffic(args.traffic, {**cfg, "erase": erase})
     achieved = enc.bytes / (enc_ms * 1e-3) / 1e9
@@ -324,11 +373,9 @@ def main(argv=None):
             "traffic": traffic,
             "traffic_source": tsrc,
             "algorithmic_bytes_per_launch": enc.bytes,
-            # also against a measured device copy of the same byte count
-            "copy_ceiling": (None if copy_gbs is None else
-                             {"kernel": "torch uint8 copy_ (read N + write N bytes)",
-                              "achieved": round(copy_gbs, 1),
-                              "frac": round(achieved / copy_gbs, 4)}),
+            # also against measured ceilings of the same traffic, live
+            "copy_ceiling": ceiling_entry(ceil, "encode", enc.bytes, achieved),
+            "nolookup": nolookup_entry(ceil, "encode", enc.bytes, achieved),
         },
         "roofline_decode": {
             "bound": "hbm",
@@ -339,13 +386,22 @@ def main(argv=None):
             "frac": round(dec_achieved / HBM_PEAK_GBS, 4),
             "traffic": dec_traffic,
             "algorithmic_bytes_per_launch": dec.bytes,
+            "copy_ceiling": ceiling_entry(ceil, "decode", dec.bytes, dec_achieved),
+            "nolookup": nolookup_entry(ceil, "decode", dec.bytes, dec_achieved),
         },
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        threads = args.cpu_threads or max(1, min(16, len(os.sched_getaffinity(0))))
+        visible = len(os.sched_getaffinity(0))
+        threads = args.cpu_threads or max(1, min(CPU_SHARE, visible))
         line["cpu_baseline"] = cpu_baseline(sb, k, m, erase, args.cpu_seconds,
                                             args.cpu_working_set, threads)
+        line["cpu_baseline"]["cores_visible"] = visible
+        if threads < visible:
+            line["cpu_baseline"]["threads_note"] = (
+                f"{threads} of {visible} visible cores: the GPU box's CPU share per GPU is "
+                f"{CPU_SHARE} (its affinity mask shows the whole host); --cpu-threads "
+                "overrides")
     if rank == 0:
         print(json.dumps(line), flush=True)
     enc.close()

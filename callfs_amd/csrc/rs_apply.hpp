@@ -796,6 +796,52 @@ void rs_apply_lds(ApplyArgs a) {
   }
 }
 
+// ---- traffic ceilings of a launch (measurement only; rs_plan_launch_ceiling) ----------
+// The launch's read streams alone (its K inputs and its Verify rows) and its write
+// streams alone (its other rows), on the production grid and tile order: 512 threads, one
+// 16-B vector per lane per shard, non-temporal, no LDS. bench.py adds the two times: the
+// HBM rate of the launch's bytes if its reads and writes each ran at their own best rate
+// one after the other, an achievable-rate denominator that does not depend on how the
+// kernel interleaves them. The read kernel stores nothing (its XOR reaches memory only if
+// it equals a value random data never gives, which keeps the loads alive); the write
+// kernel stores a lane pattern.
+template <int ORD>
+__global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + 511) / 512);
+  uint32_t stripe, tile;
+  map_tile<ORD>(a.t_base + blockIdx.x, tps, static_cast<uint32_t>(a.batch), stripe, tile);
+  const uint64_t v0 = static_cast<uint64_t>(tile) * 512 + threadIdx.x;
+  if (v0 >= a.nvec) return;
+  cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * a.K;
+  cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * a.R;
+  using P = Policy<2, 1, true, true, false, 512>;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  auto mix = [&acc](const uint4& x) {
+    acc.x ^= x.x; acc.y ^= x.y; acc.z ^= x.z; acc.w ^= x.w;
+  };
+#pragma unroll 4
+  for (int i = 0; i < a.K; ++i) mix(load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0));
+  for (int r = 0; r < a.R; ++r)
+    if ((a.verify_mask >> r) & 1u) mix(load16<P>(reinterpret_cast<const uint4*>(out[r]) + v0));
+  if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u && acc.z == 0xf39cc060u && acc.w == 0x5cedc834u)
+    a.status[0] = static_cast<int>(v0);
+}
+
+template <int ORD>
+__global__ __launch_bounds__(512) void rs_stream_write(ApplyArgs a) {
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + 511) / 512);
+  uint32_t stripe, tile;
+  map_tile<ORD>(a.t_base + blockIdx.x, tps, static_cast<uint32_t>(a.batch), stripe, tile);
+  const uint64_t v0 = static_cast<uint64_t>(tile) * 512 + threadIdx.x;
+  if (v0 >= a.nvec) return;
+  cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * a.R;
+  using P = Policy<2, 1, true, true, false, 512>;
+  const uint32_t x = static_cast<uint32_t>(v0) * 0x01000193u;
+  for (int r = 0; r < a.R; ++r)
+    if (!((a.verify_mask >> r) & 1u))
+      store16<P>(reinterpret_cast<uint4*>(out[r]) + v0, make_uint4(x, x + 1, x + 2, x + r));
+}
+
 // Dynamic LDS bytes of rs_apply_lds for K input shards and RT rows.
 inline size_t lds_bytes(int K, int RT) { return static_cast<size_t>(K) * 32 * (RT > 8 ? 16 : 8); }
 

@@ -1379,6 +1379,25 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
   return RS_OK;
 }
 
+int rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode) {
+  DeviceGuard dg;
+  if (!plan || mode < 0 || mode > 2) return RS_E_ARG;
+  HIPCHK(hipSetDevice(plan->device));
+  std::vector<int> orders;
+  {
+    std::lock_guard<std::mutex> g(plan->mu);
+    orders = plan->orders;
+  }
+  const Tables& t = *plan->tables;
+  auto* d = static_cast<uint8_t*>(plan->dmeta);
+  for (size_t gi = 0; gi < t.groups.size(); ++gi) {
+    const int order = gi < orders.size() ? orders[gi] : -1;
+    HIPCHK(launch_ceiling(group_args(t, plan->layout, gi, plan->batch, d, plan->S, 1, plan->hint),
+                          static_cast<hipStream_t>(stream), order, mode));
+  }
+  return RS_OK;
+}
+
 // Times every tile order each launch group's kernel offers and keeps the fastest. Which
 // order HBM serves best varies between MI355X boxes by 1-2 points on the same shape
 // (DESIGN.md §5 "Tile order"), so a plan that is launched many times measures it on the

@@ -403,4 +403,75 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   return hipSuccess;
 }
 
+// ---- no-lookup ceiling (measurement only; rs_plan_launch_ceiling) ----------------------
+// Policy::NOMATH turns the LDS kernel into the memory ceiling of its own traffic shape:
+// the same loads, stores, grid, block size, tile order and table prologue, with the
+// lookups replaced by one XOR per input dword (DESIGN.md §5 "Traffic ceiling per shape").
+// bench.py times it in the same process as the plan it bounds.
+namespace {
+template <int ORD, int R>
+using NomathPolicy = dev::Policy<2, 1, true, true, false, 512, (R > 8 ? 4 : 2), ORD, (R > 8 ? 1 : 0), true>;
+template <int ORD, int... Rs>
+constexpr auto nomath_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, NomathPolicy<ORD, Rs + 1>>...};
+}
+template <int ORD, int... Rs>
+constexpr auto nomath_wide_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 9, NomathPolicy<ORD, Rs + 9>>...};
+}
+// [TileOrder][R - 1] for R <= 8; wide groups: consecutive and Q8 (the orders they run)
+const std::array<std::array<VecFn, 8>, 5> kNomath = {
+    nomath_table<0>(std::make_integer_sequence<int, 8>{}), nomath_table<2>(std::make_integer_sequence<int, 8>{}),
+    nomath_table<5>(std::make_integer_sequence<int, 8>{}), nomath_table<6>(std::make_integer_sequence<int, 8>{}),
+    nomath_table<8>(std::make_integer_sequence<int, 8>{})};
+const auto kNomathWide = nomath_wide_table<0>(std::make_integer_sequence<int, 8>{});
+const auto kNomathWideQ8 = nomath_wide_table<6>(std::make_integer_sequence<int, 8>{});
+static_assert(NomathPolicy<0, 4>::TILE_VECS == LdsPolicy::TILE_VECS &&
+                  NomathPolicy<0, 16>::TILE_VECS == LdsPolicy::TILE_VECS && LdsPolicy::BS == 512,
+              "the ceilings run the production grid");
+
+const std::array<VecFn, 5> kStreamRead = {&dev::rs_stream_read<0>, &dev::rs_stream_read<2>,
+                                           &dev::rs_stream_read<5>, &dev::rs_stream_read<6>,
+                                           &dev::rs_stream_read<8>};
+const std::array<VecFn, 5> kStreamWrite = {&dev::rs_stream_write<0>, &dev::rs_stream_write<2>,
+                                            &dev::rs_stream_write<5>, &dev::rs_stream_write<6>,
+                                            &dev::rs_stream_write<8>};
+}  // namespace
+
+hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode) {
+  if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1 || !a.ltabs ||
+      mode < 0 || mode > 2)
+    return hipErrorInvalidValue;
+  a.nvec = a.S / 16;
+  if (a.nvec == 0) return hipSuccess;
+  a.tail_in_vec = a.nvec * 16 < a.S;
+  // the order the production launch would take (a tuned order, else the rule; the
+  // realigning and v_perm launches are bounded by the plain kernel's traffic)
+  const TileOrder ord =
+      a.R <= 8 ? (order >= 0 && order != kOrderRealign ? static_cast<TileOrder>(order) : lds_rule(a))
+               : (order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a));
+  const unsigned grid = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
+  if (mode > 0) {  // the read streams alone / the write streams alone
+    const VecFn fn = (mode == 1 ? kStreamRead : kStreamWrite)[static_cast<int>(ord)];
+    a.tail_in_vec = 0;
+    launch_sliced(grid, a.K + a.R, a, [&](uint32_t blocks) {
+      hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), 0, stream, a);
+    });
+    return hipGetLastError();
+  }
+  VecFn fn;
+  if (a.R <= 8)
+    fn = kNomath[static_cast<int>(ord)][a.R - 1];
+  else
+    fn = ord == TileOrder::kSeg8 ? kNomathWideQ8[a.R - 9] : kNomathWide[a.R - 9];
+  const size_t lds = dev::lds_bytes(a.K, a.R);
+  if (lds > (64u << 10))
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
+  launch_sliced(grid, a.K + a.R, a, [&](uint32_t blocks) {
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, a);
+  });
+  return hipGetLastError();
+}
+
 }  // namespace callfs

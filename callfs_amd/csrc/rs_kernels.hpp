@@ -80,6 +80,15 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false
 // no choice (byte kernel, realigning kernel, S < 16).
 std::vector<int> order_candidates(const ApplyArgs& a);
 
+// Measurement only (rs_plan_launch_ceiling), for launch `a` in the order the production
+// launch takes (`order` as for launch_apply), on the production grid and slicing:
+//   mode 0  the no-lookup form of the LDS kernel: same loads, stores and table prologue,
+//           one XOR per input dword instead of the lookups (outputs junk, Verify rows may
+//           flag status);
+//   mode 1  the launch's read streams alone (inputs + Verify rows; writes nothing);
+//   mode 2  its write streams alone (junk into the written rows).
+hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode);
+
 // rs_init: per-device setup of the kernels for each listed device (the > 64 KiB
 // dynamic-LDS opt-in of the 9..16-row instances, a per-device attribute); leaves the
 // last listed device current. launch_apply also issues it on first use per device.

@@ -95,6 +95,17 @@ class Plan:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         N.check(N.lib.rs_plan_launch(self.handle, ctypes.c_void_p(s.cuda_stream)), "rs_plan_launch")
 
+    CEILINGS = {"nolookup": 0, "read": 1, "write": 2}
+
+    def launch_ceiling(self, mode: str = "nolookup",
+                       stream: Optional[torch.cuda.Stream] = None) -> None:
+        """rs_plan_launch_ceiling (measurement only): this plan's traffic as the kernel's
+        no-lookup form, or its read / write streams alone, same grid and tile order.
+        "nolookup" and "write" leave junk in the written shards."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        N.check(N.lib.rs_plan_launch_ceiling(self.handle, ctypes.c_void_p(s.cuda_stream),
+                                             self.CEILINGS[mode]), "rs_plan_launch_ceiling")
+
     # tile orders (RS_ORDER_*); on misaligned shards 0..4 name the plain kernel with
     # unaligned accesses and "realign" the kernel that aligns loads and stores
     ORDER_NAMES = {-1: "none", 0: "consecutive", 1: "g8", 2: "g2", 3: "q8", 4: "q16", 32: "realign"}

@@ -182,6 +182,19 @@ void rs_plan_destroy(rs_plan* plan);
  * unaligned 16-B accesses in that tile order */
 #define RS_ORDER_REALIGN 32
 int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups);
+/* Measurement only (no upstream counterpart): enqueues the plan's launch groups as a
+ * traffic ceiling of the same shape, on the production grid, tile order and slicing, for
+ * a roofline denominator measured in the same process (bench.py):
+ *   RS_CEIL_NOLOOKUP  the production kernel's no-lookup form: the same loads, stores and
+ *                     table prologue, one XOR per input dword in place of the lookups;
+ *   RS_CEIL_READ      the plan's read streams alone (k inputs + compared rows);
+ *   RS_CEIL_WRITE     its write streams alone.
+ * NOLOOKUP and WRITE leave junk in the written shards and NOLOOKUP may flag status:
+ * relaunch the plan (and read rs_plan_status) before relying on either. */
+#define RS_CEIL_NOLOOKUP 0
+#define RS_CEIL_READ 1
+#define RS_CEIL_WRITE 2
+int  rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode);
 /* Launch groups of a plan (the `orders` entries rs_plan_tune can fill): one per up to 16
  * written or compared rows; 0 for a NULL plan. */
 int  rs_plan_groups(const rs_plan* plan);

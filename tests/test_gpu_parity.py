@@ -1256,3 +1256,45 @@ def test_plan_tune_misaligned_split_layout(native_lib, k, m, S, batch, off):
     dec.launch()
     assert not dec.corrupt()
     assert np.array_equal(buf.cpu().numpy()[off:off + total], host)
+
+
+@pytest.mark.parametrize("k,m,S,batch,erase", [
+    (10, 4, 1 << 20, 3, None),          # bench shape, LDS kernel R = 4
+    (10, 4, 100_003, 4, (5,)),          # one written + three compared rows, ragged tail
+    (3, 2, 349_526, 3, None),           # v_perm launch (bounded by the LDS form)
+    (10, 12, 65_536, 2, None),          # wide group R = 12
+])
+def test_plan_ceiling_modes_then_relaunch(native_lib, k, m, S, batch, erase):
+    """rs_plan_launch_ceiling (bench.py's live roofline denominators): the read-only mode
+    leaves every byte as it was; the no-lookup and write-only modes may overwrite the
+    written rows, and relaunching the plan restores them bit-exactly; bad arguments are
+    refused."""
+    import ctypes
+    import torch
+    from callfs_amd import _native as N
+    from callfs_amd.device import Plan
+    sb = _batch(k, m, S, batch, seed=S + 3 * k)
+    enc = Plan.for_batch(sb)
+    enc.launch()
+    n = k + m
+    present = None if erase is None else [i not in erase for i in range(n)]
+    plan = enc if erase is None else Plan.for_batch(sb, present=present)
+    before = sb.buf.clone()
+    plan.launch_ceiling("read")
+    torch.cuda.synchronize()
+    assert torch.equal(sb.buf, before)
+    for mode in ("write", "nolookup"):
+        plan.launch_ceiling(mode)
+        plan.corrupt()  # the no-lookup form compares junk: clear
+        plan.launch()
+        assert not plan.corrupt()
+        torch.cuda.synchronize()
+        assert torch.equal(sb.buf[:, :, :S], before[:, :, :S]), mode
+    host = sb.buf[:, :, :S].cpu().numpy()
+    want = cref.encode([host[0, i] for i in range(k)], k, m)
+    for j in range(m):
+        assert np.array_equal(host[0, k + j], want[j]), j
+    assert N.lib.rs_plan_launch_ceiling(plan.handle, None, 3) == N.RS_E_ARG
+    assert N.lib.rs_plan_launch_ceiling(None, None, 0) == N.RS_E_ARG
+    assert N.lib.rs_plan_groups(plan.handle) == max(1, -(-m // 16)) or erase is not None
+    assert N.lib.rs_plan_groups(None) == 0
