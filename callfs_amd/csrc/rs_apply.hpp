@@ -787,7 +787,10 @@ void rs_apply_lds(ApplyArgs a) {
         uint4 y;
         if constexpr (kVpf) y = vpre[r];
         else y = load16<P>(dst);
-        bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) != 0;
+        if constexpr (P::NOMATH)  // compares junk: keep the load, not a status atomic per lane
+          bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) == 0x9e3779b9u;
+        else
+          bad |= ((y.x ^ o.x) | (y.y ^ o.y) | (y.z ^ o.z) | (y.w ^ o.w)) != 0;
       } else {
         store16<P>(dst, o);
       }
@@ -819,10 +822,26 @@ __global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
   auto mix = [&acc](const uint4& x) {
     acc.x ^= x.x; acc.y ^= x.y; acc.z ^= x.z; acc.w ^= x.w;
   };
-#pragma unroll 4
-  for (int i = 0; i < a.K; ++i) mix(load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0));
-  for (int r = 0; r < a.R; ++r)
-    if ((a.verify_mask >> r) & 1u) mix(load16<P>(reinterpret_cast<const uint4*>(out[r]) + v0));
+  // 8 loads in flight per lane before any is consumed (64 VGPRs, 8 waves per SIMD)
+  for (int i0 = 0; i0 < a.K; i0 += 8) {
+    uint4 x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i0 + j < a.K) x[j] = load16<P>(reinterpret_cast<const uint4*>(in[i0 + j]) + v0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i0 + j < a.K) mix(x[j]);
+  }
+  for (int r0 = 0; r0 < a.R; r0 += 8) {
+    uint4 x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (r0 + j < a.R && ((a.verify_mask >> (r0 + j)) & 1u))
+        x[j] = load16<P>(reinterpret_cast<const uint4*>(out[r0 + j]) + v0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (r0 + j < a.R && ((a.verify_mask >> (r0 + j)) & 1u)) mix(x[j]);
+  }
   if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u && acc.z == 0xf39cc060u && acc.w == 0x5cedc834u)
     a.status[0] = static_cast<int>(v0);
 }

@@ -237,8 +237,9 @@ namespace {
 TileOrder lds_rule(const ApplyArgs& a) {
   const int forced = tile_order_override();
   if (forced >= 0) return static_cast<TileOrder>(forced);
+  const uint32_t rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
   return lds_tile_order(a.S, (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS, a.addr_tz, a.K + a.R,
-                        a.stripe_stride);
+                        a.stripe_stride, (a.verify_mask & rows) != 0);
 }
 
 TileOrder wide_rule(const ApplyArgs& a) {

@@ -66,10 +66,16 @@ enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16 };
 // Pitches with few trailing zeros (the 13-107 MB column slices of 1 GiB objects) and
 // >= 128 MiB keep consecutive tiles.
 //
+// Launch groups with Verify rows (the decodes of a download, codec.go:59) keep G2 only up
+// to 1 MiB: from 1 to 8 MiB consecutive tiles ran 0.2-1.9 points faster on every decode
+// pattern (configs[2] shape, S = 6,710,887: one erasure {5} 73.9 -> 75.2, {13} 74.3 ->
+// 75.9, nothing erased 77.4 -> 78.1; tools/ceiling_sweep.py, profiles/r03/ceil1,
+// profiles/r02/decode_order_sweep).
+//
 // tps = tiles of 512 16-B vectors (8 KiB) per stripe; streams = K + R of the launch;
-// addr_tz / stripe_stride as in ApplyArgs.
+// addr_tz / stripe_stride as in ApplyArgs; verify = the launch compares some rows.
 inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int streams,
-                                uint64_t stripe_stride) {
+                                uint64_t stripe_stride, bool verify = false) {
   // stripes exactly 2 MiB apart: interleaving stripes costs 2-12 points (RS(8,8) 128 KiB
   // 72.4 -> 60.6 with G8, RS(4,4) 256 KiB 77.9 -> 65.8, RS(6,2) 256 KiB 81.5 -> 78.4);
   // strides of 1, 4, 8 or 16 MiB interleave fine (profiles/r01/tile_order/segments/
@@ -79,7 +85,7 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
   // -> 67.7, RS(12,4) 64 KiB equal)
   if (stripe_stride == (1ull << 20) && tps <= 32) return TileOrder::kGroup2;
   if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
-  if (tps <= 128 || (tps <= 1024 && streams >= 14)) return TileOrder::kGroup2;
+  if (tps <= 128 || (tps <= 1024 && streams >= 14 && !verify)) return TileOrder::kGroup2;
   if (tps <= 1024) return TileOrder::kConsecutive;  // S <= 8 MiB, few streams
   if (addr_tz >= 23 && S < (128ull << 20)) {
     if (streams >= 12)

@@ -1,0 +1,131 @@
+"""Per-shape production rate against the live traffic ceilings (development tool).
+
+For each shape, one resident batch and one plan: the production launch (rule order, and
+optionally after rs_plan_tune), the kernel's no-lookup form, and the plan's read streams
+alone + write streams alone (rs_plan_launch_ceiling), interleaved over rounds in one
+process; every variant is warmed >= 30 ms before it is timed. Prints one JSON line per
+shape with % of 8 TB/s (algorithmic bytes / mean launch time) for each.
+
+shape spec: k,m,S,stripes[,erase[,layout]]   erase: '-' = encode, 'none' = all present,
+            or '+'-joined indices (5, 0+3+7+12); layout: 'pitch' (StripeBatch, 256-B
+            pitch, default), 'split' (upstream Split layout: object b's shard i at
+            base + (b*n + i)*S from an odd base, every shard at its own byte offset when
+            S is odd) or 'contig' (the same from an aligned base)
+usage: python tools/ceiling_sweep.py --shape 10,4,1048576,256,5 --shape ... [--tune 1]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+import torch  # noqa: E402
+
+from callfs_amd.device import Plan, StripeBatch  # noqa: E402
+
+PEAK = 8000.0
+
+
+def launch_ms(fn, stream, reps, warm_ms=30.0):
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < warm_ms:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / reps
+
+
+def build(k, m, S, B, layout, dev):
+    n = k + m
+    if layout in ("split", "contig"):
+        total = B * n * S
+        buf = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device=dev)
+        # split: odd base, so with odd S every shard sits at its own offset; contig: the
+        # same pitch = S layout from an aligned base (aligned shards when 16 | S)
+        base = buf.data_ptr() + (1 if layout == "split" else 0)
+        ptrs = [base + (b * n + i) * S for b in range(B) for i in range(n)]
+        return buf, ptrs
+    sb = StripeBatch(k, m, S, B, dev)
+    sb.fill_random(0xCA11F5)
+    return sb, sb.pointers()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", action="append", required=True)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--tune", type=int, default=0)
+    ap.add_argument("--only", default="",
+                    help="comma-separated variants to time (prod,tuned,nolookup,read,write); "
+                         "default all (rocprofv3 --pmc passes time only prod)")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    for spec in a.shape:
+        f = spec.split(",")
+        k, m, S, B = (int(x) for x in f[:4])
+        erase = f[4] if len(f) > 4 else "-"
+        layout = f[5] if len(f) > 5 else "pitch"
+        n = k + m
+        holder, ptrs = build(k, m, S, B, layout, dev)
+        enc = Plan(k, m, S, B, ptrs)
+        enc.launch(stream)
+        if erase == "-":
+            present = None
+        elif erase == "none":
+            present = [True] * n
+        else:
+            er = {int(x) for x in erase.split("+")}
+            present = [i not in er for i in range(n)]
+        plan = enc if present is None else Plan(k, m, S, B, ptrs, present=present)
+        variants = {"prod": lambda: plan.launch(stream)}
+        orders = None
+        if a.tune:
+            tuned = Plan(k, m, S, B, ptrs, present=present)
+            orders = tuned.tune(stream=stream)
+            variants["tuned"] = lambda: tuned.launch(stream)
+        for mode in ("nolookup", "read", "write"):
+            variants[mode] = (lambda md: lambda: plan.launch_ceiling(md, stream))(mode)
+        if a.only:
+            keep = set(a.only.split(","))
+            variants = {v: f for v, f in variants.items() if v in keep}
+        t = {v: [] for v in variants}
+        for r in range(a.rounds):
+            names = list(variants)
+            names = names[r % len(names):] + names[:r % len(names)]
+            for v in names:
+                t[v].append(launch_ms(variants[v], stream, a.reps))
+        plan.corrupt(stream)
+        plan.launch(stream)
+        bad = plan.corrupt(stream)
+        nb = plan.bytes
+        best = {v: min(x) for v, x in t.items()}
+        pct = {v: round(nb / (ms * 1e-3) / 1e9 / PEAK * 100, 2) for v, ms in best.items()
+               if v not in ("read", "write")}
+        if "read" in best and "write" in best:
+            rw = nb / ((best["read"] + best["write"]) * 1e-3) / 1e9 / PEAK * 100
+            pct["read+write"] = round(rw, 2)
+            if "prod" in pct:
+                pct["prod/read+write"] = round(pct["prod"] / rw, 4)
+        out = {"shape": spec, "k": k, "m": m, "S": S, "stripes": B, "erase": erase,
+               "layout": layout, "bytes": nb, "pct_of_8TBs": pct,
+               "ms": {v: round(x, 4) for v, x in best.items()}, "tuned_orders": orders,
+               "verify_after": bool(bad)}
+        print(json.dumps(out), flush=True)
+        del plan, enc, holder
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
