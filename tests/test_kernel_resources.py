@@ -40,7 +40,9 @@ def _policy(k):
 
 
 def _lds(ks):
-    return [k for k in ks if "rs_apply_lds<" in k["name"]]
+    """Production LDS-kernel instances (the NOMATH ceiling forms, Policy argument 10, are
+    measurement kernels of rs_plan_launch_ceiling and excluded)."""
+    return [k for k in ks if "rs_apply_lds<" in k["name"] and _policy(k)[9] != "true"]
 
 
 def test_every_kernel_reported(kernels):
