@@ -893,6 +893,69 @@ __global__ __launch_bounds__(kBlock) void rs_apply_bytes(ApplyArgs a, uint64_t b
   }
 }
 
+// ---- one-dispatch small calls (rs_kernels.hpp SmallArgs) -------------------------------
+// A host-memory call of a few KiB spent ~29 us in an H2D blit, the kernel and a D2H blit,
+// each a dispatch that waits for the previous one (tools/small_trace.sh: 6.6 + 7.6 + 4.2 us
+// on the GPU plus ~20 us on the host, profiles/r03/small_trace). This kernel reads the
+// lane's host-coherent staging buffer over PCIe and writes the outputs back into it: one
+// dispatch per call. Each lane owns one 16-B column vector of one stripe and issues the
+// loads of 8 input shards at a time before consuming any, so a call waits for few PCIe
+// round trips; the GF multiply is the v_perm form (tables in SGPRs, no LDS prologue).
+// Shard pitch in staging is S rounded up to 16, so the last vector of a shard covers bytes
+// past S: they are computed and stored (never copied out) and masked out of compares.
+template <int RT>
+__global__ __launch_bounds__(256) void rs_apply_small(SmallArgs a) {
+  const uint32_t v = blockIdx.x * 256u + threadIdx.x;
+  if (v >= a.nvec) return;
+  const uint8_t* s = a.base + static_cast<size_t>(blockIdx.y) * a.spitch;
+  const cptr<uint32_t> tabs = as_const(a.tabs);
+  uint32_t acc[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[r][w] = 0;
+  for (int i0 = 0; i0 < a.K; i0 += 8) {
+    uint4 x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i0 + j < a.K)
+        x[j] = *(reinterpret_cast<const uint4*>(s + a.cpitch * a.in_idx[i0 + j]) + v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (i0 + j >= a.K) break;
+      const cptr<uint32_t> t = tabs + static_cast<size_t>(i0 + j) * RT * 5;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const Sel sel = selectors(word(x[j], w));
+#pragma unroll
+        for (int r = 0; r < RT; ++r) acc[r][w] = fma1(acc[r][w], gf_mul4(sel, t + r * 5));
+      }
+    }
+  }
+  // bytes of this vector that lie inside the shard (compares ignore the rest)
+  const uint32_t live = a.S - v * 16u >= 16u ? 16u : a.S - v * 16u;
+  uint32_t mask[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t b = live > 4u * w ? live - 4u * w : 0u;
+    mask[w] = b >= 4u ? ~0u : (1u << (8u * b)) - 1u;
+  }
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    uint4* dst = reinterpret_cast<uint4*>(const_cast<uint8_t*>(s) + a.cpitch * a.out_idx[r]) + v;
+    const uint4 o = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+    if ((a.verify_mask >> r) & 1u) {
+      const uint4 y = *dst;
+      bad |= (((y.x ^ o.x) & mask[0]) | ((y.y ^ o.y) & mask[1]) | ((y.z ^ o.z) & mask[2]) |
+              ((y.w ^ o.w) & mask[3])) != 0;
+    } else {
+      *dst = o;
+    }
+  }
+  if (bad) a.status[blockIdx.y] = 1;  // every writer stores the same flag: no atomic
+}
+
 // Grid for the vector kernel: one tile per block, or (PERSIST) a fixed grid of
 // `blocks_per_cu` blocks on each of the 256 CUs.
 template <class P>

@@ -198,6 +198,29 @@ struct HostBuf {
   }
 };
 
+// Host-coherent pinned memory that kernels read and write in place (the one-dispatch
+// small-call path): the CPU fills it between calls, so device caches must not keep its
+// lines across launches (as for rs_host_alloc buffers).
+struct CoherentBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return RS_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    n = std::max<size_t>(n, 64u << 10);
+    if (hipHostMalloc(&p, n, hipHostMallocCoherent) != hipSuccess) return RS_E_NOMEM;
+    cap = n;
+    return RS_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 // Layout facts the kernel dispatch keys its tile order on (ApplyArgs addr_tz,
 // stripe_stride).
 struct LayoutHint {
@@ -222,6 +245,12 @@ struct Slot {
   LayoutHint meta_hint;  // of the pointers in `meta`
   void* meta_base = nullptr;
   HostBuf hstat;         // per-stripe verify flags of the chunk in flight
+  // one-dispatch small calls: staging the kernel works on in place (+ status words),
+  // and the v_perm tables of the tables set it was last used with, per launch group
+  CoherentBuf small;
+  DevBuf small_tabs;
+  std::shared_ptr<const Tables> small_tables;
+  std::vector<size_t> small_tab_off;
   bool pending = false;  // a chunk's outputs wait in `host`
   int b0 = 0, count = 0;  // its stripes
   size_t off = 0, width = 0;  // and columns
@@ -244,6 +273,16 @@ size_t chunk_bytes() {
     const char* e = std::getenv("CALLFS_RS_CHUNK_BYTES");
     const long long x = e ? std::atoll(e) : 0;
     return x >= (64 << 10) ? static_cast<size_t>(x) : (16u << 20);
+  }();
+  return v;
+}
+
+// Calls moving at most this many staging bytes (n shards rounded to 16 B, all stripes)
+// take the one-dispatch small path (CALLFS_RS_SMALL_MAX_BYTES overrides; 0 turns it off).
+size_t small_max_bytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("CALLFS_RS_SMALL_MAX_BYTES");
+    return e ? static_cast<size_t>(std::strtoull(e, nullptr, 0)) : (256u << 10);
   }();
   return v;
 }
@@ -513,6 +552,8 @@ struct rs_ctx {
           sl.meta.release();
           sl.hmeta.release();
           sl.hstat.release();
+          sl.small.release();
+          sl.small_tabs.release();
           if (sl.done) (void)hipEventDestroy(sl.done);
           if (sl.stream) (void)hipStreamDestroy(sl.stream);
         }
@@ -799,6 +840,82 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
           if (stripe_status) stripe_status[b] = 1;
         }
     }
+    return corrupt ? RS_E_CORRUPT : RS_OK;
+  }
+
+  // One dispatch per call for small calls: copy the inputs into the lane's host-coherent
+  // staging, one rs_apply_small launch per launch group reads and writes it over PCIe, one
+  // event wait, copy the outputs out. The staged path spends three dependent dispatches
+  // (H2D, kernel, D2H) per chunk, which bound 4 KiB calls at ~29 us.
+  const size_t cp16 = round_up(S, 16), sp16 = cp16 * n;
+  if (sp16 * static_cast<size_t>(batch) <= small_max_bytes() && batch <= 65535 &&
+      S <= 0xFFFFFFF0u) {
+    Slot& sl = L.slot[0];
+    const size_t stat_off = round_up(sp16 * batch, 256);
+    int rc;
+    if ((rc = sl.small.ensure(stat_off + sizeof(int) * batch))) return rc;
+    if (sl.small_tables != tp) {
+      std::vector<size_t> off;
+      size_t tot = 0;
+      for (const Group& g : t.groups) {
+        off.push_back(tot);
+        tot = round_up(tot + g.tabs.size() * sizeof(uint32_t), 256);
+      }
+      sl.small_tables = nullptr;
+      if ((rc = sl.small_tabs.ensure(tot))) return rc;
+      for (size_t gi = 0; gi < t.groups.size(); ++gi)
+        HIPCHK(hipMemcpyAsync(static_cast<uint8_t*>(sl.small_tabs.p) + off[gi],
+                              t.groups[gi].tabs.data(),
+                              t.groups[gi].tabs.size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, sl.stream));
+      sl.small_tables = tp;
+      sl.small_tab_off = off;
+    }
+    auto* base = static_cast<uint8_t*>(sl.small.p);
+    int* st = reinterpret_cast<int*>(base + stat_off);
+    std::vector<CopyPool::Seg> segs;
+    for (int b = 0; b < batch; ++b)
+      for (int i : ins) {
+        const auto tee = join_span(join, i, col0, S);
+        segs.push_back({base + sp16 * b + cp16 * i, host_in(b, i), S, tee.first, tee.second});
+      }
+    ctx->pool.run(segs);
+    if (verify) std::memset(st, 0, sizeof(int) * batch);
+    for (size_t gi = 0; gi < t.groups.size(); ++gi) {
+      const Group& g = t.groups[gi];
+      SmallArgs A{};
+      A.base = base;
+      A.spitch = sp16;
+      A.cpitch = cp16;
+      A.nvec = static_cast<uint32_t>(cp16 / 16);
+      A.S = static_cast<uint32_t>(S);
+      A.K = t.k;
+      A.R = static_cast<int>(g.shard.size());
+      A.batch = batch;
+      A.verify_mask = g.verify_mask;
+      A.tabs = reinterpret_cast<const uint32_t*>(static_cast<uint8_t*>(sl.small_tabs.p) +
+                                                 sl.small_tab_off[gi]);
+      A.status = st;
+      for (int i = 0; i < t.k; ++i) A.in_idx[i] = static_cast<uint8_t>(t.valid[i]);
+      for (int r = 0; r < A.R; ++r) A.out_idx[r] = static_cast<uint8_t>(g.shard[r]);
+      HIPCHK(launch_small(A, sl.stream));
+    }
+    HIPCHK(hipEventRecord(sl.done, sl.stream));
+    HIPCHK(hipEventSynchronize(sl.done));
+    bool corrupt = false;
+    if (verify)
+      for (int b = 0; b < batch; ++b)
+        if (st[b]) {
+          corrupt = true;
+          if (stripe_status) stripe_status[b] = 1;
+        }
+    segs.clear();
+    for (int b = 0; b < batch; ++b)
+      for (int i : outs) {
+        const auto tee = join_span(join, i, col0, S);
+        segs.push_back({host_out(b, i), base + sp16 * b + cp16 * i, S, tee.first, tee.second});
+      }
+    ctx->pool.run(segs);
     return corrupt ? RS_E_CORRUPT : RS_OK;
   }
 

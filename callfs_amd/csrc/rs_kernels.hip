@@ -218,6 +218,25 @@ void wide_lds_opt_in(int R) {
 
 }  // namespace
 
+namespace {
+using SmallFn = void (*)(SmallArgs);
+template <int... Rs>
+constexpr auto small_table(std::integer_sequence<int, Rs...>) {
+  return std::array<SmallFn, sizeof...(Rs)>{&dev::rs_apply_small<Rs + 1>...};
+}
+const auto kSmall = small_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
+}  // namespace
+
+hipError_t launch_small(const SmallArgs& a, hipStream_t stream) {
+  if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1 ||
+      a.batch > 65535 || a.nvec == 0 || !a.base || !a.tabs || !a.status)
+    return hipErrorInvalidValue;
+  const unsigned gx = (a.nvec + 255u) / 256u;
+  hipLaunchKernelGGL(kSmall[a.R - 1], dim3(gx, static_cast<unsigned>(a.batch)), dim3(256), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
 bool prepare_devices(const std::vector<int>& devices) {
   return setup_devices(
       devices, g_wide_lds, kWideKeys, [](int d) { return hipSetDevice(d) == hipSuccess; },

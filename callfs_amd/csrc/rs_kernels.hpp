@@ -50,6 +50,28 @@ struct ApplyArgs {
   uint32_t tail_in_vec;
 };
 
+// One-dispatch small host calls (rs_apply_small): stripe b's shard i lives at
+// base + b*spitch + i*cpitch in host-coherent pinned staging that the kernel reads and
+// writes over PCIe; one launch group (R <= 16 rows) per launch.
+struct SmallArgs {
+  const uint8_t* base;
+  uint64_t spitch;       // bytes per stripe in staging
+  uint64_t cpitch;       // bytes per shard (S rounded up to 16)
+  uint32_t nvec;         // 16-B vectors per shard, ceil(S / 16)
+  uint32_t S;
+  int K;
+  int R;
+  int batch;
+  uint32_t verify_mask;
+  const uint32_t* tabs;  // device memory: [K][R][5] v_perm tables of the group
+  int* status;           // host-coherent: status[b] = 1 when stripe b's Verify rows mismatch
+  uint8_t in_idx[256];   // shard index of input i (the k valid shards)
+  uint8_t out_idx[16];   // shard index of row r (written or compared)
+};
+
+// Enqueues rs_apply_small for one launch group on `stream`.
+hipError_t launch_small(const SmallArgs& a, hipStream_t stream);
+
 // addr_tz for a set of shard addresses: trailing zeros of the OR of their differences
 // from the first (63 for a single address).
 inline int shard_addr_tz(const void* const* p, int count) {
