@@ -61,6 +61,11 @@ def parse_args(argv=None):
                    help="configs[3] mode: objects of this size (e.g. 1073741824) split by byte "
                         "columns across the ranks (strong scaling); --stripes objects in total")
     p.add_argument("--erase", default="0,1,2,3", help="erased shard indices for decode")
+    p.add_argument("--split-layout", action="store_true",
+                   help="upstream Split layout (codec.go:31): each object's n shards "
+                        "contiguous at pitch = S, objects back to back (configs[1]: "
+                        "--shard-bytes 6710887, misaligned shards at odd S) instead of the "
+                        "256-B shard pitch")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="CPU baseline time budget (0 disables)")
     p.add_argument("--cpu-working-set", type=int, default=2 << 30,
@@ -263,7 +268,7 @@ def main(argv=None):
     erase = sorted({int(x) for x in args.erase.split(",") if x != ""})
     present = [i not in erase for i in range(k + m)]
 
-    sb = StripeBatch(k, m, S, B, dev)
+    sb = StripeBatch(k, m, S, B, dev, layout="split" if args.split_layout else "pitch")
     sb.fill_random(0xCA11F5 + rank)
     enc = Plan.for_batch(sb)
     dec = Plan.for_batch(sb, present=present)
@@ -325,6 +330,8 @@ def main(argv=None):
         raise SystemExit("verify flagged corruption during the timed run")
     ceil = plan_ceilings(enc, dec, stream) if args.ceiling else None
     cfg = {"k": k, "m": m, "shard_bytes": S, "stripes": B}
+    if args.split_layout:
+        cfg["layout"] = "split"
     traffic, dec_traffic, tsrc = load_traffic(args.traffic, {**cfg, "erase": erase})
     achieved = enc.bytes / (enc_ms * 1e-3) / 1e9
     dec_achieved = dec.bytes / (dec_ms * 1e-3) / 1e9
@@ -345,7 +352,9 @@ def main(argv=None):
         "config": {
             "workload": (f"RS({k},{m}) device-resident encode + decode(erase {erase}), "
                          + (f"{B} objects of {args.object_bytes} B split by byte columns over "
-                            f"{world} GPU(s)" if S_obj else f"{S} B shards, {B} stripes per GPU")),
+                            f"{world} GPU(s)" if S_obj else f"{S} B shards, {B} stripes per GPU")
+                         + (", upstream Split layout (pitch = S, contiguous objects)"
+                            if args.split_layout else "")),
             **cfg,
             "erase": erase,
             # decode re-verifies only the present parity beyond the first k (a9): none

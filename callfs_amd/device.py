@@ -25,12 +25,21 @@ def pitch_for(S: int) -> int:
 
 
 class StripeBatch:
-    """`batch` stripes of RS(k, m) with shard size S, resident on `device`."""
+    """`batch` stripes of RS(k, m) with shard size S, resident on `device`.
 
-    def __init__(self, k: int, m: int, S: int, batch: int, device: torch.device):
+    layout "pitch" (default): shards at a 256-B pitch, every shard 16-B aligned.
+    layout "split": upstream `Split`'s layout of contiguous objects (codec.go:31):
+    pitch = S, object b's shard i at b*n*S + i*S, so at odd S every shard but the
+    first sits at its own byte offset (the realigning kernel's case)."""
+
+    def __init__(self, k: int, m: int, S: int, batch: int, device: torch.device,
+                 layout: str = "pitch"):
+        if layout not in ("pitch", "split"):
+            raise ValueError(f"layout {layout!r}")
         self.k, self.m, self.S, self.batch = k, m, S, batch
         self.n = k + m
-        self.pitch = pitch_for(S)
+        self.layout = layout
+        self.pitch = pitch_for(S) if layout == "pitch" else S
         self.device = torch.device(device)
         self.buf = torch.empty((batch, self.n, self.pitch), dtype=torch.uint8, device=self.device)
 

@@ -7,7 +7,7 @@ cd "$R"
 export CALLFS_RS_TUNE_LOG=1
 for i in 1 2 3; do
   for t in 1 0; do
-    timeout -k 10 300 python3 bench.py --cpu-seconds 0 --copy-ceiling 0 --tune $t "$@" > "$OUT/bench_${i}_tune$t.log" 2>&1 || exit $?
+    timeout -k 10 300 python3 bench.py --cpu-seconds 0 --ceiling 0 --tune $t "$@" > "$OUT/bench_${i}_tune$t.log" 2>&1 || exit $?
     echo "run $i tune=$t: $(grep rs_plan_tune "$OUT/bench_${i}_tune$t.log" | tr '\n' ' ')"
     tail -1 "$OUT/bench_${i}_tune$t.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('  value', d['value'], 'enc', d['roofline']['frac'], 'dec', d['roofline_decode']['frac'], d['config']['tile_order'])"
   done
