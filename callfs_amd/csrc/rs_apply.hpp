@@ -898,32 +898,47 @@ __global__ __launch_bounds__(kBlock) void rs_apply_bytes(ApplyArgs a, uint64_t b
 // each a dispatch that waits for the previous one (tools/small_trace.sh: 6.6 + 7.6 + 4.2 us
 // on the GPU plus ~20 us on the host, profiles/r03/small_trace). This kernel reads the
 // lane's host-coherent staging buffer over PCIe and writes the outputs back into it: one
-// dispatch per call. Each lane owns one 16-B column vector of one stripe and issues the
-// loads of 8 input shards at a time before consuming any, so a call waits for few PCIe
-// round trips; the GF multiply is the v_perm form (tables in SGPRs, no LDS prologue).
+// dispatch per call. Each lane owns one 16-B column vector of one stripe, so a call waits
+// for few PCIe round trips; the GF multiply is the v_perm form (tables in SGPRs, no LDS prologue).
+// 16 loads are issued before any is consumed (one PCIe round trip for k <= 16).
 // Shard pitch in staging is S rounded up to 16, so the last vector of a shard covers bytes
 // past S: they are computed and stored (never copied out) and masked out of compares.
 template <int RT>
-__global__ __launch_bounds__(256) void rs_apply_small(SmallArgs a) {
-  const uint32_t v = blockIdx.x * 256u + threadIdx.x;
-  if (v >= a.nvec) return;
+__device__ __forceinline__ void small_vector(const SmallArgs& a, uint32_t v) {
   const uint8_t* s = a.base + static_cast<size_t>(blockIdx.y) * a.spitch;
   const cptr<uint32_t> tabs = as_const(a.tabs);
+  // shard indices as dwords (scalar loads; byte loads would be per-lane vector loads, each
+  // waited for before the data load it addresses)
+  const cptr<uint32_t> idx = as_const(reinterpret_cast<const uint32_t*>(a.idx));
   uint32_t acc[RT][4];
 #pragma unroll
   for (int r = 0; r < RT; ++r)
 #pragma unroll
     for (int w = 0; w < 4; ++w) acc[r][w] = 0;
-  for (int i0 = 0; i0 < a.K; i0 += 8) {
-    uint4 x[8];
+  // 16 loads in flight before any is consumed: a call with k <= 16 waits for one PCIe round
+  // trip of reads. Loads past K re-read shard K-1 (unconditional loads keep them in flight
+  // together; their values are not used).
+  for (int i0 = 0; i0 < a.K; i0 += 16) {
+    uint32_t iw[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (i0 + j < a.K)
-        x[j] = *(reinterpret_cast<const uint4*>(s + a.cpitch * a.in_idx[i0 + j]) + v);
+    for (int q = 0; q < 4; ++q) iw[q] = i0 == 0 ? a.idx_in[q] : idx[(i0 >> 2) + q];
+    const uint32_t lw = a.K <= 16 ? a.idx_in[(a.K - 1) >> 2] : idx[(a.K - 1) >> 2];
+    const uint32_t last = lw >> (8 * ((a.K - 1) & 3)) & 0xffu;
+    uint4 x[16];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (i0 + j >= a.K) break;
-      const cptr<uint32_t> t = tabs + static_cast<size_t>(i0 + j) * RT * 5;
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t sh = i0 + j < a.K ? (iw[j >> 2] >> (8 * (j & 3))) & 0xffu : last;
+      x[j] = *(reinterpret_cast<const uint4*>(s + a.cpitch * sh) + v);
+    }
+    // keep the 16 loads ahead of every use (left alone, the scheduler sank each load next
+    // to its consumer: 16 PCIe round trips one after another)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      // past K: input 0 through shard K-1's tables adds nothing (no branch in the loop)
+      const bool in = i0 + j < a.K;
+      if (!in) x[j] = make_uint4(0, 0, 0, 0);
+      const cptr<uint32_t> t = tabs + static_cast<size_t>(in ? i0 + j : a.K - 1) * RT * 5;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
         const Sel sel = selectors(word(x[j], w));
@@ -943,7 +958,8 @@ __global__ __launch_bounds__(256) void rs_apply_small(SmallArgs a) {
   bool bad = false;
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
-    uint4* dst = reinterpret_cast<uint4*>(const_cast<uint8_t*>(s) + a.cpitch * a.out_idx[r]) + v;
+    const uint32_t row = (a.idx_out[r >> 2] >> (8 * (r & 3))) & 0xffu;
+    uint4* dst = reinterpret_cast<uint4*>(const_cast<uint8_t*>(s) + a.cpitch * row) + v;
     const uint4 o = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
     if ((a.verify_mask >> r) & 1u) {
       const uint4 y = *dst;
@@ -954,6 +970,29 @@ __global__ __launch_bounds__(256) void rs_apply_small(SmallArgs a) {
     }
   }
   if (bad) a.status[blockIdx.y] = 1;  // every writer stores the same flag: no atomic
+}
+
+// The completion flag (SmallArgs::done): the host spins on it instead of waiting for the
+// runtime's completion signal, which returned ~5 us after the kernel had ended
+// (tools/small_trace.sh). Every block makes its stores visible system-wide, then counts
+// itself done on a device-memory counter; the last block resets the counter and releases
+// the call's sequence number into the host flag.
+template <int RT>
+__global__ __launch_bounds__(256) void rs_apply_small(SmallArgs a) {
+  const uint32_t v = blockIdx.x * 256u + threadIdx.x;
+  if (v < a.nvec) small_vector<RT>(a, v);
+  if (a.done) {  // launch-uniform
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence_system();
+      const unsigned total = gridDim.x * gridDim.y;
+      if (atomicAdd(a.counter, 1u) == total - 1u) {
+        atomicExch(a.counter, 0u);
+        __threadfence_system();
+        __hip_atomic_store(a.done, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
 }
 
 // Grid for the vector kernel: one tile per block, or (PERSIST) a fixed grid of

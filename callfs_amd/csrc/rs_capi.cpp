@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <atomic>
 #include <condition_variable>
@@ -248,6 +249,8 @@ struct Slot {
   // one-dispatch small calls: staging the kernel works on in place (+ status words),
   // and the v_perm tables of the tables set it was last used with, per launch group
   CoherentBuf small;
+  DevBuf small_counter;  // finished-block counter of the completion flag
+  int small_seq = 0;     // sequence number of the last small call on this slot
   DevBuf small_tabs;
   std::shared_ptr<const Tables> small_tables;
   std::vector<size_t> small_tab_off;
@@ -282,9 +285,23 @@ size_t chunk_bytes() {
 size_t small_max_bytes() {
   static const size_t v = [] {
     const char* e = std::getenv("CALLFS_RS_SMALL_MAX_BYTES");
-    return e ? static_cast<size_t>(std::strtoull(e, nullptr, 0)) : (256u << 10);
+    return e ? static_cast<size_t>(std::strtoull(e, nullptr, 0)) : (2u << 20);
   }();
   return v;
+}
+
+// Host spin on a flag a kernel releases with a system-scope store (rs_apply_small):
+// true once *flag == want, false after `us` microseconds.
+constexpr int kSmallSpinUs = 2000;
+bool spin_until(const int* flag, int want, int us) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 0;; ++i) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == want) return true;
+    if ((i & 63u) == 63u &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(us))
+      return false;
+    __builtin_ia32_pause();
+  }
 }
 
 struct Lane {
@@ -554,6 +571,7 @@ struct rs_ctx {
           sl.hstat.release();
           sl.small.release();
           sl.small_tabs.release();
+          sl.small_counter.release();
           if (sl.done) (void)hipEventDestroy(sl.done);
           if (sl.stream) (void)hipStreamDestroy(sl.stream);
         }
@@ -852,27 +870,40 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
       S <= 0xFFFFFFF0u) {
     Slot& sl = L.slot[0];
     const size_t stat_off = round_up(sp16 * batch, 256);
+    const size_t done_off = round_up(stat_off + sizeof(int) * batch, 256);
     int rc;
-    if ((rc = sl.small.ensure(stat_off + sizeof(int) * batch))) return rc;
+    if ((rc = sl.small.ensure(done_off + 256))) return rc;
+    if (!sl.small_counter.p) {
+      if ((rc = sl.small_counter.ensure(256))) return rc;
+      HIPCHK(hipMemset(sl.small_counter.p, 0, 256));
+    }
     if (sl.small_tables != tp) {
+      // per launch group: [v_perm tables][idx: 256 input + 16 row shard indices]
       std::vector<size_t> off;
       size_t tot = 0;
       for (const Group& g : t.groups) {
         off.push_back(tot);
-        tot = round_up(tot + g.tabs.size() * sizeof(uint32_t), 256);
+        tot = round_up(tot + g.tabs.size() * sizeof(uint32_t) + 272, 256);
       }
       sl.small_tables = nullptr;
       if ((rc = sl.small_tabs.ensure(tot))) return rc;
-      for (size_t gi = 0; gi < t.groups.size(); ++gi)
-        HIPCHK(hipMemcpyAsync(static_cast<uint8_t*>(sl.small_tabs.p) + off[gi],
-                              t.groups[gi].tabs.data(),
-                              t.groups[gi].tabs.size() * sizeof(uint32_t),
-                              hipMemcpyHostToDevice, sl.stream));
+      std::vector<uint8_t> h(tot, 0);
+      for (size_t gi = 0; gi < t.groups.size(); ++gi) {
+        const Group& g = t.groups[gi];
+        const size_t tb = g.tabs.size() * sizeof(uint32_t);
+        std::memcpy(h.data() + off[gi], g.tabs.data(), tb);
+        uint8_t* ix = h.data() + off[gi] + tb;
+        for (int i = 0; i < t.k; ++i) ix[i] = static_cast<uint8_t>(t.valid[i]);
+        for (size_t r = 0; r < g.shard.size(); ++r) ix[256 + r] = static_cast<uint8_t>(g.shard[r]);
+      }
+      HIPCHK(hipMemcpy(sl.small_tabs.p, h.data(), tot, hipMemcpyHostToDevice));
       sl.small_tables = tp;
       sl.small_tab_off = off;
     }
     auto* base = static_cast<uint8_t*>(sl.small.p);
     int* st = reinterpret_cast<int*>(base + stat_off);
+    int* done = reinterpret_cast<int*>(base + done_off);
+    const int seq = ++sl.small_seq == 0 ? ++sl.small_seq : sl.small_seq;
     std::vector<CopyPool::Seg> segs;
     for (int b = 0; b < batch; ++b)
       for (int i : ins) {
@@ -893,15 +924,24 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
       A.R = static_cast<int>(g.shard.size());
       A.batch = batch;
       A.verify_mask = g.verify_mask;
-      A.tabs = reinterpret_cast<const uint32_t*>(static_cast<uint8_t*>(sl.small_tabs.p) +
-                                                 sl.small_tab_off[gi]);
+      const uint8_t* tb = static_cast<uint8_t*>(sl.small_tabs.p) + sl.small_tab_off[gi];
+      A.tabs = reinterpret_cast<const uint32_t*>(tb);
+      A.idx = tb + g.tabs.size() * sizeof(uint32_t);
+      for (int i = 0; i < std::min(t.k, 16); ++i)
+        A.idx_in[i >> 2] |= static_cast<uint32_t>(t.valid[i]) << (8 * (i & 3));
+      for (size_t r = 0; r < g.shard.size(); ++r)
+        A.idx_out[r >> 2] |= static_cast<uint32_t>(g.shard[r]) << (8 * (r & 3));
       A.status = st;
-      for (int i = 0; i < t.k; ++i) A.in_idx[i] = static_cast<uint8_t>(t.valid[i]);
-      for (int r = 0; r < A.R; ++r) A.out_idx[r] = static_cast<uint8_t>(g.shard[r]);
+      const bool last = gi + 1 == t.groups.size();
+      A.done = last ? done : nullptr;
+      A.counter = static_cast<unsigned*>(sl.small_counter.p);
+      A.seq = seq;
       HIPCHK(launch_small(A, sl.stream));
     }
-    HIPCHK(hipEventRecord(sl.done, sl.stream));
-    HIPCHK(hipEventSynchronize(sl.done));
+    // spin on the kernel's completion flag (~5 us sooner than the runtime's signal); past
+    // kSmallSpinUs, or if the launch failed, fall back to the stream wait, which also
+    // reports a faulted kernel
+    if (!spin_until(done, seq, kSmallSpinUs)) HIPCHK(hipStreamSynchronize(sl.stream));
     bool corrupt = false;
     if (verify)
       for (int b = 0; b < batch; ++b)

@@ -229,7 +229,7 @@ const auto kSmall = small_table(std::make_integer_sequence<int, kMaxRowsPerLaunc
 
 hipError_t launch_small(const SmallArgs& a, hipStream_t stream) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1 ||
-      a.batch > 65535 || a.nvec == 0 || !a.base || !a.tabs || !a.status)
+      a.batch > 65535 || a.nvec == 0 || !a.base || !a.tabs || !a.idx || !a.status)
     return hipErrorInvalidValue;
   const unsigned gx = (a.nvec + 255u) / 256u;
   hipLaunchKernelGGL(kSmall[a.R - 1], dim3(gx, static_cast<unsigned>(a.batch)), dim3(256), 0,

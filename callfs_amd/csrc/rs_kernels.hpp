@@ -63,10 +63,23 @@ struct SmallArgs {
   int R;
   int batch;
   uint32_t verify_mask;
-  const uint32_t* tabs;  // device memory: [K][R][5] v_perm tables of the group
+  // device memory, uploaded once per (lane, tables): [K][R][5] v_perm tables of the group,
+  // then idx: the shard index of input i (idx[i], the k valid shards) and of row r
+  // (idx[256 + r]). Kept out of the kernel arguments: 272 B of arguments cost the launch
+  // ~2 us (tools/small_trace.sh)
+  const uint32_t* tabs;
+  const uint8_t* idx;
+  // idx[0..15] and idx[256..271] again, as kernel arguments: the data loads of a k <= 16
+  // call need no dependent device-memory read first
+  uint32_t idx_in[4];
+  uint32_t idx_out[4];
   int* status;           // host-coherent: status[b] = 1 when stripe b's Verify rows mismatch
-  uint8_t in_idx[256];   // shard index of input i (the k valid shards)
-  uint8_t out_idx[16];   // shard index of row r (written or compared)
+  // completion flag (last launch of a call only, else null): when every block of the launch
+  // has finished, the last one stores `seq` into *done (host-coherent) with a system-scope
+  // release; `counter` (device memory, 0 between launches) counts finished blocks
+  int* done;
+  unsigned* counter;
+  int seq;
 };
 
 // Enqueues rs_apply_small for one launch group on `stream`.

@@ -79,14 +79,14 @@ __global__ __launch_bounds__(512) void lds_rate(const uint32_t* seed, uint32_t* 
 }
 
 template <int W>
-void run(const uint32_t* seed, uint32_t* out, int blocks, int iters, double ghz) {
+void run(const uint32_t* seed, uint32_t* out, int blocks, int iters, double ghz, size_t dyn) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(lds_rate<W>, dim3(blocks), dim3(512), 0, 0, seed, out, iters);
+  for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(lds_rate<W>, dim3(blocks), dim3(512), dyn, 0, seed, out, iters);
   CK(hipEventRecord(a));
   const int reps = 5;
-  for (int rep = 0; rep < reps; ++rep) hipLaunchKernelGGL(lds_rate<W>, dim3(blocks), dim3(512), 0, 0, seed, out, iters);
+  for (int rep = 0; rep < reps; ++rep) hipLaunchKernelGGL(lds_rate<W>, dim3(blocks), dim3(512), dyn, 0, seed, out, iters);
   CK(hipEventRecord(b));
   CK(hipEventSynchronize(b));
   float ms = 0;
@@ -94,9 +94,9 @@ void run(const uint32_t* seed, uint32_t* out, int blocks, int iters, double ghz)
   const double lookups = static_cast<double>(blocks) * 512 * iters * 32 * reps;  // 16 bytes x 2
   const double s = ms * 1e-3;
   const double bytes = lookups * W;
-  std::printf("{\"W\": %d, \"lookups_per_s\": %.4g, \"lds_TBps\": %.2f, \"bytes_per_cu_clk_at_%.1fGHz\": %.1f, "
+  std::printf("{\"W\": %d, \"waves_per_simd\": %d, \"lookups_per_s\": %.4g, \"lds_TBps\": %.2f, \"bytes_per_cu_clk_at_%.1fGHz\": %.1f, "
               "\"data_bytes_per_s_TB\": %.2f}\n",
-              W, lookups / s, bytes / s / 1e12, ghz, bytes / s / 256 / (ghz * 1e9), lookups / 2 / s / 1e12);
+              W, dyn ? static_cast<int>(8 * ((160u << 10) / (dyn + 8192)) / 4) : 8, lookups / s, bytes / s / 1e12, ghz, bytes / s / 256 / (ghz * 1e9), lookups / 2 / s / 1e12);
 }
 
 int main(int argc, char** argv) {
@@ -109,8 +109,18 @@ int main(int argc, char** argv) {
   uint32_t* h = static_cast<uint32_t*>(std::malloc(sizeof(uint32_t) * blocks * 512 * 4));
   for (size_t i = 0; i < static_cast<size_t>(blocks) * 512 * 4; ++i) h[i] = static_cast<uint32_t>(i * 2246822519u + 3266489917u);
   CK(hipMemcpy(seed, h, sizeof(uint32_t) * blocks * 512 * 4, hipMemcpyHostToDevice));
-  run<4>(seed, out, blocks, iters, ghz);
-  run<8>(seed, out, blocks, iters, ghz);
-  run<16>(seed, out, blocks, iters, ghz);
+  // dynamic LDS padding limits blocks per CU: 0 -> 4 blocks (8 waves per SIMD), 64 KiB ->
+  // 2 blocks (4 waves per SIMD), 40 KiB -> 3 blocks (6 waves per SIMD)
+  for (size_t dyn : {static_cast<size_t>(0), static_cast<size_t>(40u << 10), static_cast<size_t>(64u << 10)}) {
+    if (dyn > (64u << 10)) continue;
+    if (dyn) {
+      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate<4>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate<8>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate<16>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+    }
+    run<4>(seed, out, blocks, iters, ghz, dyn);
+    run<8>(seed, out, blocks, iters, ghz, dyn);
+    run<16>(seed, out, blocks, iters, ghz, dyn);
+  }
   return 0;
 }

@@ -6,7 +6,7 @@ R="$GRAFT_REPO_ROOT"; TAG="${1:-smallpath}"; OUT="$R/gpurun_out/$TAG"; mkdir -p 
 export CALLFS_E2E_ENCODER=1
 for prof in "16 4 0,5,16,19" "4 2 1,4"; do
   set -- $prof
-  for L in 4096 16384 65536 262144 1048576; do
+  for L in ${SIZES:-4096 16384 65536 262144 1048576}; do
     for t in 1 8; do
       for mode in staged small; do
         lim=$([ $mode = staged ] && echo 0 || echo 67108864)

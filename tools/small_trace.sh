@@ -5,7 +5,7 @@ set -o pipefail
 R="$GRAFT_REPO_ROOT"; TAG="${1:-smalltrace}"; OUT="$R/gpurun_out/$TAG"; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 export CALLFS_E2E_ENCODER=1
-for lim in 0 262144; do
+for lim in 0 2097152; do
   CALLFS_RS_SMALL_MAX_BYTES=$lim timeout -k 10 60 "$R/tools/e2e_native" 16 4 4096 1 1.0 0,5,16,19 > "$OUT/plain_$lim.jsonl" 2>&1 || exit $?
   CALLFS_RS_SMALL_MAX_BYTES=$lim timeout -k 10 120 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d "$OUT/trace_$lim" -o tr -- \
     "$R/tools/e2e_native" 16 4 4096 1 0.3 0,5,16,19 > "$OUT/traced_$lim.jsonl" 2>&1 || exit $?
