@@ -17,7 +17,7 @@
   do {                                                                         \
     hipError_t e = (x);                                                        \
     if (e != hipSuccess) {                                                     \
-      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      std::printf("error %s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
       std::exit(1);                                                            \
     }                                                                          \
   } while (0)
@@ -84,6 +84,7 @@ void run(const uint32_t* seed, uint32_t* out, int blocks, int iters, double ghz,
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(lds_rate<W>, dim3(blocks), dim3(512), dyn, 0, seed, out, iters);
+  CK(hipGetLastError());
   CK(hipEventRecord(a));
   const int reps = 5;
   for (int rep = 0; rep < reps; ++rep) hipLaunchKernelGGL(lds_rate<W>, dim3(blocks), dim3(512), dyn, 0, seed, out, iters);
@@ -114,9 +115,9 @@ int main(int argc, char** argv) {
   for (size_t dyn : {static_cast<size_t>(0), static_cast<size_t>(40u << 10), static_cast<size_t>(64u << 10)}) {
     if (dyn > (64u << 10)) continue;
     if (dyn) {
-      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate<4>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
-      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate<8>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
-      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate<16>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate<4>), hipFuncAttributeMaxDynamicSharedMemorySize, (160 << 10) - 8192));
+      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate<8>), hipFuncAttributeMaxDynamicSharedMemorySize, (160 << 10) - 8192));
+      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate<16>), hipFuncAttributeMaxDynamicSharedMemorySize, (160 << 10) - 8192));
     }
     run<4>(seed, out, blocks, iters, ghz, dyn);
     run<8>(seed, out, blocks, iters, ghz, dyn);
