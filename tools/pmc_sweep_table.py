@@ -22,7 +22,7 @@ def main(d):
         spec = open(shp).read().strip()
         vals = {}
         nbytes = None
-        for p in range(4):
+        for p in range(6):
             log = os.path.join(d, f"s{i}_p{p}.log")
             if nbytes is None and os.path.exists(log):
                 for ln in open(log):
@@ -47,6 +47,12 @@ def main(d):
             out["write_bytes"] = vals["WRITE_SIZE"] * 1024
         if nbytes and "fetch_bytes" in out and "write_bytes" in out:
             out["traffic_over_algorithmic"] = round((out["fetch_bytes"] + out["write_bytes"]) / nbytes, 4)
+        if vals.get("TCC_EA0_RDREQ_LEVEL_sum") and vals.get("TCC_EA0_RDREQ_sum"):
+            # Little's law: mean read requests outstanding x cycles / requests = mean
+            # memory-side read latency in L2 cycles
+            out["read_latency_tcc_cycles"] = round(vals["TCC_EA0_RDREQ_LEVEL_sum"] / vals["TCC_EA0_RDREQ_sum"], 1)
+        if vals.get("TCC_EA0_WRREQ_LEVEL_sum") and vals.get("TCC_EA0_WRREQ_sum"):
+            out["write_latency_tcc_cycles"] = round(vals["TCC_EA0_WRREQ_LEVEL_sum"] / vals["TCC_EA0_WRREQ_sum"], 1)
         out["counters"] = vals
         rows.append(out)
         print(json.dumps(out))
