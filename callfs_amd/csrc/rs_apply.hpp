@@ -132,7 +132,6 @@ struct Policy {
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 template <class P>
 __device__ __forceinline__ uint4 load16(const uint4* p) {
@@ -808,7 +807,14 @@ void rs_apply_lds(ApplyArgs a) {
 // one after the other, an achievable-rate denominator that does not depend on how the
 // kernel interleaves them. The read kernel stores nothing (its XOR reaches memory only if
 // it equals a value random data never gives, which keeps the loads alive); the write
-// kernel stores a lane pattern.
+// kernel stores a lane pattern. On a misaligned batch (Split layout) both time aligned
+// 16-B accesses -- the traffic the realigning kernel issues -- not unaligned ones: reads
+// from each shard's base rounded down to 16 B (same page), stores from its first 16-B
+// boundary on, inside the shard.
+__device__ __forceinline__ const uint4* align16(const uint8_t* p) {
+  return reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+}
+
 template <int ORD>
 __global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
   const uint32_t tps = static_cast<uint32_t>((a.nvec + 511) / 512);
@@ -828,7 +834,7 @@ __global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
     uint4 x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (i0 + j < a.K) x[j] = load16<P>(reinterpret_cast<const uint4*>(in[i0 + j]) + v0);
+      if (i0 + j < a.K) x[j] = load16<P>(align16(in[i0 + j]) + v0);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (i0 + j < a.K) mix(x[j]);
@@ -838,7 +844,7 @@ __global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (r0 + j < a.R && ((a.verify_mask >> (r0 + j)) & 1u))
-        x[j] = load16<P>(reinterpret_cast<const uint4*>(out[r0 + j]) + v0);
+        x[j] = load16<P>(align16(out[r0 + j]) + v0);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (r0 + j < a.R && ((a.verify_mask >> (r0 + j)) & 1u)) mix(x[j]);
@@ -858,118 +864,14 @@ __global__ __launch_bounds__(512) void rs_stream_write(ApplyArgs a) {
   using P = Policy<2, 1, true, true, false, 512>;
   const uint32_t x = static_cast<uint32_t>(v0) * 0x01000193u;
   for (int r = 0; r < a.R; ++r)
-    if (!((a.verify_mask >> r) & 1u))
-      store16<P>(reinterpret_cast<uint4*>(out[r]) + v0, make_uint4(x, x + 1, x + 2, x + r));
-}
-
-// ---- wide groups, 8 bytes per lane (experiment: CALLFS_RS_WIDE_HALF=1) -----------------
-// R 9..16 at 16-B entries hold 16 byte positions x 16 rows of accumulators per lane (64
-// VGPRs) and run 4 waves per SIMD. With 8 bytes per lane the accumulators halve, so more
-// waves fit and more LDS lookups and HBM loads are in flight per CU, at twice the memory
-// instructions per byte (8-B global accesses). Same tables, tile order and ragged-tail
-// handling as rs_apply_lds; a tile is 512 lanes x 8 B.
-template <int RT, bool SD>
-__device__ __forceinline__ void lds_mac_half(u32x4_acc (&acc)[2][4], const uint2& x, uint32_t base) {
-  static_assert(RT > 8, "16-byte entries");
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    const uint32_t xw = w == 0 ? x.x : x.y;
-    const uint32_t xl = (xw << 4) & 0xf0f0f0f0u, xh = xw & 0xf0f0f0f0u;
-    const uint32_t base_hi = base + 256u;
-    u32x4_acc lo[4], hi[4];
-    if constexpr (SD) {
-      const uint32_t sb = __builtin_amdgcn_readfirstlane(base);
-      const uint32_t sbh = __builtin_amdgcn_readfirstlane(base_hi);
-      lo[0] = lds_lookup<RT>(or_byte<0>(xl, sb));
-      hi[0] = lds_lookup<RT>(or_byte<0>(xh, sbh));
-      lo[1] = lds_lookup<RT>(or_byte<1>(xl, sb));
-      hi[1] = lds_lookup<RT>(or_byte<1>(xh, sbh));
-      lo[2] = lds_lookup<RT>(or_byte<2>(xl, sb));
-      hi[2] = lds_lookup<RT>(or_byte<2>(xh, sbh));
-      lo[3] = lds_lookup<RT>(or_byte<3>(xl, sb));
-      hi[3] = lds_lookup<RT>(or_byte<3>(xh, sbh));
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t sel = 0x07060500u | static_cast<uint32_t>(j);
-        lo[j] = lds_lookup<RT>(__builtin_amdgcn_perm(base, xl, sel));
-        hi[j] = lds_lookup<RT>(__builtin_amdgcn_perm(base_hi, xh, sel));
-      }
+    if (!((a.verify_mask >> r) & 1u)) {
+      // aligned blocks inside the row: from the first 16-B boundary at or after its base,
+      // one block fewer when the base is misaligned (never a byte outside [base, base + S))
+      const uintptr_t q = reinterpret_cast<uintptr_t>(out[r]);
+      const uintptr_t up = (q + 15) & ~uintptr_t(15);
+      if (up != q && v0 + 1 >= a.nvec) continue;
+      store16<P>(reinterpret_cast<uint4*>(up) + v0, make_uint4(x, x + 1, x + 2, x + r));
     }
-    __builtin_amdgcn_sched_group_barrier(0x0100, 8, 0);
-    __builtin_amdgcn_sched_group_barrier(0x0002, 64, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[w][j] = lds_x3(acc[w][j], lo[j], hi[j]);
-  }
-}
-
-template <int RT, class P>
-__global__ __launch_bounds__(P::BS) __attribute__((amdgpu_waves_per_eu(P::WPE, 8)))
-void rs_apply_lds_half(ApplyArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr int BS = P::BS;
-  constexpr int W = 16;
-  const int K = a.K;
-  const int R = a.R;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(a.ltabs);
-    uint4* dst = reinterpret_cast<uint4*>(smem);
-    for (int j = threadIdx.x; j < K * 2 * W; j += BS) dst[j] = src[j];
-  }
-  __syncthreads();
-  const uint32_t lds0 = static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)smem));
-  const uint64_t nunit = a.nvec * 2;  // 8-B units in [0, 16 nvec)
-  const uint32_t tps = static_cast<uint32_t>((nunit + BS - 1) / BS);
-  const uint32_t ntiles = tps * static_cast<uint32_t>(a.batch);
-  for (uint32_t t = a.t_base + blockIdx.x; t < ntiles; t += ntiles) {
-    uint32_t stripe, tile;
-    map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
-    const uint64_t u0 = static_cast<uint64_t>(tile) * BS + threadIdx.x;
-    cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
-    cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
-    if (tile == 0 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
-    if (u0 >= nunit) continue;
-    auto ld = [&](int i) {
-      const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(in[i]) + u0);
-      return make_uint2(v.x, v.y);
-    };
-    u32x4_acc acc[2][4];
-#pragma unroll
-    for (int w = 0; w < 2; ++w)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[w][j] = lds_zero<RT>();
-    constexpr int PD = P::PD, NR = P::PD + 1;
-    uint2 xr[NR];
-#pragma unroll
-    for (int q = 0; q < PD; ++q) xr[q] = q < K ? ld(q) : make_uint2(0, 0);
-#pragma unroll 1
-    for (int i0 = 0; i0 < K; i0 += NR) {
-#pragma unroll
-      for (int q = 0; q < NR; ++q) {
-        const int i = i0 + q;
-        if (i < K) {
-          if (i + PD < K) xr[(q + PD) % NR] = ld(i + PD);
-          lds_mac_half<RT, P::SDWA>(acc, xr[q], lds0 + static_cast<uint32_t>(i) * 32u * W);
-        }
-      }
-    }
-    bool bad = false;
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      if (r >= R) continue;
-      const uint2 o = make_uint2(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r));
-      u32x2* dst = reinterpret_cast<u32x2*>(out[r]) + u0;
-      if ((a.verify_mask >> r) & 1u) {
-        const u32x2 y = __builtin_nontemporal_load(dst);
-        bad |= ((y.x ^ o.x) | (y.y ^ o.y)) != 0;
-      } else {
-        const u32x2 w2 = {o.x, o.y};
-        __builtin_nontemporal_store(w2, dst);
-      }
-    }
-    if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
-  }
 }
 
 // Dynamic LDS bytes of rs_apply_lds for K input shards and RT rows.

@@ -201,22 +201,6 @@ constexpr auto lds_wide_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 9, P>...};
 }
 const auto kLdsWideQ8 = lds_wide_table<LdsWideQ8Policy>(std::make_integer_sequence<int, 8>{});
-// experiment (CALLFS_RS_WIDE_HALF=1): 8 bytes per lane for R 9..16 (rs_apply_lds_half)
-using LdsHalfPolicy = dev::Policy<2, 1, true, true, false, 512, 4, 0, 1, false, false, true>;
-using LdsHalfQ8Policy = dev::Policy<2, 1, true, true, false, 512, 4, 6, 1, false, false, true>;
-template <class P, int... Rs>
-constexpr auto lds_half_table(std::integer_sequence<int, Rs...>) {
-  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds_half<Rs + 9, P>...};
-}
-const auto kLdsHalf = lds_half_table<LdsHalfPolicy>(std::make_integer_sequence<int, 8>{});
-const auto kLdsHalfQ8 = lds_half_table<LdsHalfQ8Policy>(std::make_integer_sequence<int, 8>{});
-bool wide_half() {
-  static const bool on = [] {
-    const char* e = std::getenv("CALLFS_RS_WIDE_HALF");
-    return e && *e == '1';
-  }();
-  return on;
-}
 const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>{});
 
 // Row groups of 9..16 with more than 64 KiB of tables (k > 128) need the dynamic-LDS
@@ -227,7 +211,7 @@ DeviceOnce g_wide_lds;
 constexpr int kWideKeys = kMaxRowsPerLaunch - 8;
 
 void wide_lds_opt_in(int R) {
-  for (VecFn f : {kLds[R - 1], kLdsWideQ8[R - 9], kLdsHalf[R - 9], kLdsHalfQ8[R - 9]})
+  for (VecFn f : {kLds[R - 1], kLdsWideQ8[R - 9]})
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
 }
@@ -396,11 +380,6 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
                           LdsRealignOut8Policy::TILE_VECS == LdsRealignOutPolicy::TILE_VECS,
                       "one grid shape for every LDS policy");
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
-        if (a.R > 8 && wide_half()) {  // experiment: 8 bytes per lane, twice the tiles
-          fn = fn == kLdsWideQ8[a.R - 9] ? kLdsHalfQ8[a.R - 9] : kLdsHalf[a.R - 9];
-          gx = static_cast<unsigned>((2 * a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS *
-                                     static_cast<uint64_t>(a.batch));
-        }
         // misaligned shards: the realigning form, unless a tuned order names a plain kernel
         if (can_realign(a) && (order == kOrderRealign || (order < 0 && takes_realign(a)))) {
           fn = kLdsRealignOut[a.R - 1];

@@ -1298,3 +1298,29 @@ def test_plan_ceiling_modes_then_relaunch(native_lib, k, m, S, batch, erase):
     assert N.lib.rs_plan_launch_ceiling(None, None, 0) == N.RS_E_ARG
     assert N.lib.rs_plan_groups(plan.handle) == max(1, -(-m // 16)) or erase is not None
     assert N.lib.rs_plan_groups(None) == 0
+
+
+@pytest.mark.parametrize("k,m,S,batch", [(10, 4, 100_003, 3), (4, 2, 65_537, 5)])
+def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m, S, batch):
+    """On an upstream Split-layout batch (misaligned shards, pitch = S) the ceiling modes
+    change nothing but the written shards: the write-only mode stores aligned blocks from
+    each row's first 16-B boundary on, never a byte of a neighbouring input shard; the
+    plan then restores its outputs bit-exactly."""
+    import torch
+    from callfs_amd.device import Plan, StripeBatch
+    sb = StripeBatch(k, m, S, batch, torch.device("cuda:0"), layout="split")
+    sb.fill_random(S + k)
+    enc = Plan.for_batch(sb)
+    enc.launch()
+    before = sb.buf.clone()
+    for mode in ("read", "write", "nolookup"):
+        enc.launch_ceiling(mode)
+        torch.cuda.synchronize()
+        assert torch.equal(sb.buf[:, :k], before[:, :k]), mode  # inputs untouched
+        enc.launch()
+        torch.cuda.synchronize()
+        assert torch.equal(sb.buf, before), mode
+    host = sb.buf.cpu().numpy()
+    want = cref.encode([host[batch - 1, i] for i in range(k)], k, m)
+    for j in range(m):
+        assert np.array_equal(host[batch - 1, k + j], want[j]), j
