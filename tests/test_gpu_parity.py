@@ -1324,3 +1324,23 @@ def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m,
     want = cref.encode([host[batch - 1, i] for i in range(k)], k, m)
     for j in range(m):
         assert np.array_equal(host[batch - 1, k + j], want[j]), j
+
+
+@pytest.mark.parametrize("k,m,L", [(10, 4, 10 * 1000 + 7), (4, 2, 4 * 37 + 1), (16, 4, 4096)])
+def test_small_path_verify_masks_the_tail_vector(codec, k, m, L):
+    """Small calls take the one-dispatch path, whose last 16-B vector per shard runs past S
+    (padding in staging): a flipped last byte of a compared parity shard must be reported,
+    while the padding is never compared (clean decodes of odd-S objects stay clean)."""
+    from callfs_amd import ErasureProfile, ErrShardCorrupted
+    p = ErasureProfile(k, m)
+    data = rnd(L + k, L)
+    full = [bytes(s) for s in codec.encode(data, p)]
+    S = len(full[0])
+    sh = [None if i == 0 else full[i] for i in range(k + m)]
+    assert codec.decode(sh, p, L) == data  # k-1 data + m parity: m-1 compared rows, clean
+    for pos in (S - 1, 0):
+        bad = [bytearray(x) for x in full]
+        bad[k + m - 1][pos] ^= 0x80
+        sh = [None if i == 0 else bad[i] for i in range(k + m)]
+        with pytest.raises(ErrShardCorrupted):
+            codec.decode(sh, p, L)
