@@ -115,15 +115,11 @@ struct Policy {
   // LDS table addresses by v_or_b32_sdwa (byte select + OR) instead of v_perm_b32
   static constexpr bool SDWA = SDWA_;
   // 0: plain; 1: aligned loads realigned in registers (63 vectors per wave); 2: loads and
-  // parity stores both aligned (62 vectors per wave, edge bytes in the first tile); 3: as 2,
-  // with each wave's edge vectors handed to the previous wave through LDS (64 per wave)
+  // parity stores both aligned (62 vectors per wave, edge bytes in the first tile)
   static constexpr int REALIGN = REALIGN_;
   // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads
-  // (REALIGN 3: waves of 64 aligned vectors; the neighbour of each wave's last lane comes
-  // from the next wave through LDS, so a tile of 512 loads stores 510 aligned blocks)
-  static constexpr int WAVE_VECS = REALIGN_ == 2 ? 62 : (REALIGN_ == 1 || PROBE_ == 1) ? 63 : 64;
-  static constexpr int TILE_VECS =
-      REALIGN_ == 3 ? BS_ - 2 : WAVE_VECS < 64 ? BS_ / 64 * WAVE_VECS : BS_ * U_;
+  static constexpr int WAVE_VECS = REALIGN_ == 2 ? 62 : (REALIGN_ || PROBE_ == 1) ? 63 : 64;
+  static constexpr int TILE_VECS = WAVE_VECS < 64 ? BS_ / 64 * WAVE_VECS : BS_ * U_;
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
   static constexpr bool NT_LOAD = NT_LOAD_;
@@ -377,17 +373,6 @@ __device__ __forceinline__ uint4 shift_from_next(const uint4& A, uint32_t d) {
   if (d == 0) return A;  // wave-uniform
   const uint4 B = make_uint4(from_next_lane(A.x), from_next_lane(A.y), from_next_lane(A.z),
                              from_next_lane(A.w));
-  const uint32_t r = d & 3u;
-  switch (d >> 2) {  // wave-uniform
-    case 0: return funnel16<0>(A, B, r);
-    case 1: return funnel16<1>(A, B, r);
-    case 2: return funnel16<2>(A, B, r);
-    default: return funnel16<3>(A, B, r);
-  }
-}
-
-// Bytes d..15 of A followed by bytes 0..d-1 of B (d wave-uniform, 1..15).
-__device__ __forceinline__ uint4 funnel_by(const uint4& A, const uint4& B, uint32_t d) {
   const uint32_t r = d & 3u;
   switch (d >> 2) {  // wave-uniform
     case 0: return funnel16<0>(A, B, r);
@@ -688,27 +673,20 @@ void rs_apply_lds(ApplyArgs a) {
     map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
     // REALIGN: wave w of the tile produces vectors tile*TV + 63w + lane (lanes 0..62)
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
     constexpr uint32_t WV = P::WAVE_VECS;
-    constexpr uint32_t NWAVE = BS / 64;
-    const uint64_t v0 = P::REALIGN == 3 ? static_cast<uint64_t>(tile) * TV + threadIdx.x
-                        : WV < 64 ? static_cast<uint64_t>(tile) * TV + wave * WV + lane
-                                  : static_cast<uint64_t>(tile) * BS + threadIdx.x;
+    const uint64_t v0 = WV < 64 ? static_cast<uint64_t>(tile) * TV + (threadIdx.x >> 6) * WV + lane
+                                : static_cast<uint64_t>(tile) * BS + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
-    if constexpr (P::REALIGN >= 2) {
+    if constexpr (P::REALIGN == 2) {
       if (tile == 0) lds_edges<RT>(a, in, out, stripe, lds0);
     } else {
       if (tile == 0 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
     }
     // lanes that store (REALIGN: lane 63 -- REALIGN 2: lanes 62, 63 -- and lanes past the
     // shard only load)
-    // REALIGN 3: the block's last wave stores lanes 0..61 (lane 62's block needs lane 63's
-    // result, whose neighbour belongs to the next tile)
-    const bool active = v0 < a.nvec && (P::REALIGN == 3 ? (wave + 1 < NWAVE || lane < 62u) : lane < WV) &&
-                        !(P::PROBE == 2 && lane == 63u);
-    // REALIGN: whole wave idle; REALIGN 3 never skips (its waves meet at barriers)
-    if (P::REALIGN == 3 ? false : P::REALIGN ? (v0 - lane >= a.nvec) : !active) continue;
+    const bool active = v0 < a.nvec && lane < WV && !(P::PROBE == 2 && lane == 63u);
+    if (P::REALIGN ? (v0 - lane >= a.nvec) : !active) continue;  // REALIGN: whole wave idle
     auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
     AccT acc[4][4];
 #pragma unroll
@@ -724,35 +702,7 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll
     for (int r = 0; r < (kVpf ? RT : 1); ++r) vpre[r] = make_uint4(0, 0, 0, 0);
 
-    if constexpr (P::REALIGN == 3) {
-      static_assert(!P::NOMATH, "REALIGN: no NOMATH form");
-      // ring of three aligned vectors; a misaligned shard's vector is realigned with the
-      // next lane's (DPP), and each wave's lane 63 takes the next wave's lane 0 vector from
-      // LDS (exchange slots after the tables, double-buffered by exchange count; every
-      // exchange is one block barrier, taken by all waves since the shard is block-uniform)
-      uint4* xs = reinterpret_cast<uint4*>(smem + static_cast<size_t>(K) * 32 * W);
-      auto lda = [&](int i) { return ld_aligned<P>(in[i], v0, a.nvec); };
-      uint4 x0 = lda(0), x1 = K > 1 ? lda(1) : x0, x2 = x0;
-      uint32_t xb = 0;
-#pragma unroll 1
-      for (int i = 0; i < K; ++i) {
-        if (i + 2 < K) x2 = lda(i + 2);
-        const uint32_t d = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(in[i])) & 15u;
-        uint4 xv = x0;
-        if (d) {  // block-uniform
-          uint4 nb = make_uint4(from_next_lane(x0.x), from_next_lane(x0.y), from_next_lane(x0.z),
-                                from_next_lane(x0.w));
-          if (lane == 0) xs[xb * NWAVE + wave] = x0;
-          __syncthreads();
-          if (lane == 63u && wave + 1 < NWAVE) nb = xs[xb * NWAVE + wave + 1];
-          xb ^= 1u;
-          xv = funnel_by(x0, nb, d);
-        }
-        lds_mac<RT, P::SDWA>(acc, xv, lds0 + static_cast<uint32_t>(i) * 32u * W);
-        x0 = x1;
-        x1 = x2;
-      }
-    } else if constexpr (P::REALIGN) {
+    if constexpr (P::REALIGN) {
       static_assert(!P::NOMATH, "REALIGN: no NOMATH form");
       // ring of three aligned vectors, realigned when consumed
       auto lda = [&](int i) { return ld_aligned<P>(in[i], v0, a.nvec); };
@@ -812,40 +762,12 @@ void rs_apply_lds(ApplyArgs a) {
     }
 
     bool bad = false;
-    // REALIGN 3: each wave's lane 0 results go to LDS for the previous wave's lane 63 (the
-    // aligned store of a misaligned row needs result v + 1); one barrier for all rows
-    uint4* xo = reinterpret_cast<uint4*>(smem + static_cast<size_t>(K) * 32 * W) + 2 * NWAVE;
-    if constexpr (P::REALIGN == 3) {
-      if (lane == 0) {
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-          if (r < R)
-            xo[r * NWAVE + wave] = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
-                                              lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
-      }
-      __syncthreads();
-    }
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       if (r >= R) continue;  // wave-uniform
       const uint4 o = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
                                  lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
       uint4* dst = reinterpret_cast<uint4*>(out[r]) + v0;
-      if constexpr (P::REALIGN == 3) {
-        if (!((a.verify_mask >> r) & 1u)) {
-          const uint32_t mo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r])) & 15u;
-          if (mo) {  // block-uniform: aligned block at out[r] + f + 16 v0
-            const uint32_t f = 16u - mo;
-            uint4 nb = make_uint4(from_next_lane(o.x), from_next_lane(o.y), from_next_lane(o.z),
-                                  from_next_lane(o.w));
-            if (lane == 63u && wave + 1 < NWAVE) nb = xo[r * NWAVE + wave + 1];
-            const uint4 O = funnel_by(o, nb, f);
-            if (active && v0 + 1 < a.nvec)
-              store16<P>(reinterpret_cast<uint4*>(out[r] + f) + v0, O);
-            continue;
-          }
-        }
-      }
       if constexpr (P::REALIGN == 2) {
         if (!((a.verify_mask >> r) & 1u)) {
           const uint32_t mo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r])) & 15u;
@@ -954,9 +876,6 @@ __global__ __launch_bounds__(512) void rs_stream_write(ApplyArgs a) {
 
 // Dynamic LDS bytes of rs_apply_lds for K input shards and RT rows.
 inline size_t lds_bytes(int K, int RT) { return static_cast<size_t>(K) * 32 * (RT > 8 ? 16 : 8); }
-// REALIGN 3 adds its exchange slots after the tables: 2 x 8 input vectors + 8 rows x 8
-// result vectors (512-thread blocks)
-constexpr size_t kRealign3Xchg = (2 * 8 + 8 * 8) * 16;
 
 // One byte position per lane over [b0, S): ragged tails (S % 16).
 template <int RT>

@@ -83,13 +83,6 @@ using LdsRealignOut8Policy = dev::Policy<8, 1, true, true, false, 512, 2, 0, 0, 
 template <int R>
 using LdsRealignOutPolicyFor =
     typename std::conditional<(R <= 4), LdsRealignOut8Policy, LdsRealignOutPolicy>::type;
-// REALIGN 3 (CALLFS_RS_REALIGN=3, A/B): 64 aligned vectors per wave, each wave's edge
-// vectors handed over through LDS at one block barrier per misaligned shard
-using LdsRealign3Policy = dev::Policy<2, 1, true, true, false, 512, 2, 0, 0, false, 3>;
-using LdsRealign38Policy = dev::Policy<8, 1, true, true, false, 512, 2, 0, 0, false, 3>;
-template <int R>
-using LdsRealign3PolicyFor =
-    typename std::conditional<(R <= 4), LdsRealign38Policy, LdsRealign3Policy>::type;
 // CALLFS_RS_TILE_ORDER=consecutive|g8|g2|q8|q16 overrides the rule for every LDS-kernel
 // launch with R <= 8 (A/B on a deployment's own shard layout; unset = the rule).
 int tile_order_override() {
@@ -203,11 +196,6 @@ constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1>>...};
 }
 const auto kLdsRealignOut = lds_realign_out_table(std::make_integer_sequence<int, 8>{});
-template <int... Rs>
-constexpr auto lds_realign3_table(std::integer_sequence<int, Rs...>) {
-  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealign3PolicyFor<Rs + 1>>...};
-}
-const auto kLdsRealign3 = lds_realign3_table(std::make_integer_sequence<int, 8>{});
 template <class P, int... Rs>
 constexpr auto lds_wide_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 9, P>...};
@@ -287,14 +275,6 @@ bool realign_out_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("CALLFS_RS_REALIGN");
     return !(e && *e == '0');
-  }();
-  return on;
-}
-// CALLFS_RS_REALIGN=3 selects the REALIGN 3 form for misaligned launches (A/B)
-bool realign3() {
-  static const bool on = [] {
-    const char* e = std::getenv("CALLFS_RS_REALIGN");
-    return e && *e == '3';
   }();
   return on;
 }
@@ -397,25 +377,18 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
                           LdsWideQ8Policy::BS == LdsPolicy::BS &&
                           LdsVerifyPolicy<0>::TILE_VECS == LdsPolicy::TILE_VECS &&
                           LdsRealignOutPolicy::BS == LdsPolicy::BS &&
-                          LdsRealignOut8Policy::TILE_VECS == LdsRealignOutPolicy::TILE_VECS &&
-                          LdsRealign3Policy::BS == 512 && LdsRealign38Policy::TILE_VECS == LdsRealign3Policy::TILE_VECS,
+                          LdsRealignOut8Policy::TILE_VECS == LdsRealignOutPolicy::TILE_VECS,
                       "one grid shape for every LDS policy");
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         // misaligned shards: the realigning form, unless a tuned order names a plain kernel
-        size_t lds_launch = lds;
         if (can_realign(a) && (order == kOrderRealign || (order < 0 && takes_realign(a)))) {
           fn = kLdsRealignOut[a.R - 1];
           gx = dev::vec_grid<LdsRealignOutPolicy>(a.nvec, a.batch);
-          if (realign3() && lds + dev::kRealign3Xchg <= (64u << 10)) {
-            fn = kLdsRealign3[a.R - 1];
-            gx = dev::vec_grid<LdsRealign3Policy>(a.nvec, a.batch);
-            lds_launch = lds + dev::kRealign3Xchg;
-          }
           a.tail_in_vec = 1;  // its first tile writes every edge byte, the tail included
           tail0 = a.S;
         }
         launch_sliced(gx, a.K + a.R, a, [&](uint32_t blocks) {
-          hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds_launch, stream, a);
+          hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, a);
         });
       } else {
         a.tail_in_vec = tail0 < a.S;  // as for the LDS kernel: the first tile takes the tail
