@@ -9,7 +9,7 @@ for prof in "16 4 0,5,16,19" "4 2 1,4"; do
   for L in ${SIZES:-4096 16384 65536 262144 1048576}; do
     for t in 1 8; do
       for mode in staged small; do
-        lim=$([ $mode = staged ] && echo 0 || echo 67108864)
+        lim=$([ $mode = staged ] && echo 0 || echo ${SMALL_LIM:-67108864})
         echo "{\"mode\": \"$mode\", \"small_max\": $lim}" >> $O
         CALLFS_RS_SMALL_MAX_BYTES=$lim timeout -k 10 60 "$R/tools/e2e_native" $1 $2 $L $t 0.6 $3 >> $O || exit 1
       done
