@@ -904,6 +904,8 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     int* st = reinterpret_cast<int*>(base + stat_off);
     int* done = reinterpret_cast<int*>(base + done_off);
     const int seq = ++sl.small_seq == 0 ? ++sl.small_seq : sl.small_seq;
+    // a fresh or moved buffer holds whatever it held: clear the flag before the launch
+    __atomic_store_n(done, 0, __ATOMIC_RELEASE);
     std::vector<CopyPool::Seg> segs;
     for (int b = 0; b < batch; ++b)
       for (int i : ins) {
