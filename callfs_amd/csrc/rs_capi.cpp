@@ -290,6 +290,16 @@ size_t small_max_bytes() {
   return v;
 }
 
+// CALLFS_RS_INPLACE_PIPELINE=1: calls above the small limit run the chunk pipeline with
+// in-place kernels on host-coherent staging instead of H2D / kernel / D2H (A/B)
+bool inplace_pipeline() {
+  static const bool on = [] {
+    const char* e = std::getenv("CALLFS_RS_INPLACE_PIPELINE");
+    return e && *e == '1';
+  }();
+  return on;
+}
+
 // Host spin on a flag a kernel releases with a system-scope store (rs_apply_small):
 // true once *flag == want, false after `us` microseconds.
 constexpr int kSmallSpinUs = 2000;
@@ -753,6 +763,76 @@ std::vector<std::pair<int, int>> index_runs(std::vector<int> v) {
   return runs;
 }
 
+// In-place kernels on host-coherent staging (rs_apply_small): make `sl` ready for
+// tables `tp` with `bytes` of staging -- the v_perm tables and shard indices of every
+// launch group uploaded to device memory once per (slot, tables), and the finished-block
+// counter of the completion flag.
+int prep_inplace(Slot& sl, const std::shared_ptr<const Tables>& tp, size_t bytes) {
+  int rc;
+  if ((rc = sl.small.ensure(bytes))) return rc;
+  if (!sl.small_counter.p) {
+    if ((rc = sl.small_counter.ensure(256))) return rc;
+    HIPCHK(hipMemset(sl.small_counter.p, 0, 256));
+  }
+  if (sl.small_tables == tp) return RS_OK;
+  const Tables& t = *tp;
+  // per launch group: [v_perm tables][idx: 256 input + 16 row shard indices]
+  std::vector<size_t> off;
+  size_t tot = 0;
+  for (const Group& g : t.groups) {
+    off.push_back(tot);
+    tot = round_up(tot + g.tabs.size() * sizeof(uint32_t) + 272, 256);
+  }
+  sl.small_tables = nullptr;
+  if ((rc = sl.small_tabs.ensure(tot))) return rc;
+  std::vector<uint8_t> h(tot, 0);
+  for (size_t gi = 0; gi < t.groups.size(); ++gi) {
+    const Group& g = t.groups[gi];
+    const size_t tb = g.tabs.size() * sizeof(uint32_t);
+    std::memcpy(h.data() + off[gi], g.tabs.data(), tb);
+    uint8_t* ix = h.data() + off[gi] + tb;
+    for (int i = 0; i < t.k; ++i) ix[i] = static_cast<uint8_t>(t.valid[i]);
+    for (size_t r = 0; r < g.shard.size(); ++r) ix[256 + r] = static_cast<uint8_t>(g.shard[r]);
+  }
+  HIPCHK(hipMemcpy(sl.small_tabs.p, h.data(), tot, hipMemcpyHostToDevice));
+  sl.small_tables = tp;
+  sl.small_tab_off = off;
+  return RS_OK;
+}
+
+// One chunk in place: `cnt` stripes at base + b*sp, shard i at + i*cp, w bytes per shard;
+// the last launch group releases `seq` into *done when all its blocks have finished.
+hipError_t launch_inplace(Slot& sl, const Tables& t, uint8_t* base, size_t sp, size_t cp,
+                          size_t w, int cnt, int* st, int* done, int seq) {
+  for (size_t gi = 0; gi < t.groups.size(); ++gi) {
+    const Group& g = t.groups[gi];
+    SmallArgs A{};
+    A.base = base;
+    A.spitch = sp;
+    A.cpitch = cp;
+    A.nvec = static_cast<uint32_t>((w + 15) / 16);
+    A.S = static_cast<uint32_t>(w);
+    A.K = t.k;
+    A.R = static_cast<int>(g.shard.size());
+    A.batch = cnt;
+    A.verify_mask = g.verify_mask;
+    const uint8_t* tb = static_cast<uint8_t*>(sl.small_tabs.p) + sl.small_tab_off[gi];
+    A.tabs = reinterpret_cast<const uint32_t*>(tb);
+    A.idx = tb + g.tabs.size() * sizeof(uint32_t);
+    for (int i = 0; i < std::min(t.k, 16); ++i)
+      A.idx_in[i >> 2] |= static_cast<uint32_t>(t.valid[i]) << (8 * (i & 3));
+    for (size_t r = 0; r < g.shard.size(); ++r)
+      A.idx_out[r >> 2] |= static_cast<uint32_t>(g.shard[r]) << (8 * (r & 3));
+    A.status = st;
+    A.done = gi + 1 == t.groups.size() ? done : nullptr;
+    A.counter = static_cast<unsigned*>(sl.small_counter.p);
+    A.seq = seq;
+    const hipError_t e = launch_small(A, sl.stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 template <class InF, class OutF>
 int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const Tables>& tp,
                   size_t S, int batch, InF host_in, OutF host_out, int* stripe_status,
@@ -861,103 +941,92 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
     return corrupt ? RS_E_CORRUPT : RS_OK;
   }
 
-  // One dispatch per call for small calls: copy the inputs into the lane's host-coherent
-  // staging, one rs_apply_small launch per launch group reads and writes it over PCIe, one
-  // event wait, copy the outputs out. The staged path spends three dependent dispatches
-  // (H2D, kernel, D2H) per chunk, which bound 4 KiB calls at ~29 us.
+  // In-place kernels on host-coherent staging (rs_apply_small): the kernel reads the
+  // inputs and writes the outputs over PCIe, one dispatch per chunk and launch group, and
+  // the host spins on the kernel's completion flag. The staged path spends three dependent
+  // dispatches (H2D, kernel, D2H) per chunk, which bound 4 KiB calls at ~29 us
+  // (DESIGN.md §6.3). Calls of at most CALLFS_RS_SMALL_MAX_BYTES of staging run as one
+  // chunk on slot 0; with CALLFS_RS_INPLACE_PIPELINE=1 (A/B) larger calls run the staged
+  // path's chunk pipeline with in-place kernels instead of H2D / kernel / D2H.
   const size_t cp16 = round_up(S, 16), sp16 = cp16 * n;
-  if (sp16 * static_cast<size_t>(batch) <= small_max_bytes() && batch <= 65535 &&
-      S <= 0xFFFFFFF0u) {
-    Slot& sl = L.slot[0];
-    const size_t stat_off = round_up(sp16 * batch, 256);
-    const size_t done_off = round_up(stat_off + sizeof(int) * batch, 256);
-    int rc;
-    if ((rc = sl.small.ensure(done_off + 256))) return rc;
-    if (!sl.small_counter.p) {
-      if ((rc = sl.small_counter.ensure(256))) return rc;
-      HIPCHK(hipMemset(sl.small_counter.p, 0, 256));
+  const bool one_chunk = sp16 * static_cast<size_t>(batch) <= small_max_bytes() &&
+                         batch <= 65535 && S <= 0xFFFFFFF0u;
+  if (one_chunk || (inplace_pipeline() && cw <= 0xFFFFFFF0u && spc <= 65535)) {
+    // chunk geometry: the whole call, or the staged path's chunks
+    const size_t icw = one_chunk ? S : cw, icp = round_up(icw, 16), isp = icp * n;
+    const int ispc = one_chunk ? batch : spc;
+    const size_t incol = one_chunk ? 1 : ncol, inblk = one_chunk ? 1 : nblk;
+    const size_t ichunks = incol * inblk;
+    const int islots = one_chunk ? 1 : static_cast<int>(std::min<size_t>(ichunks, kSlots));
+    const size_t stat_off = round_up(isp * ispc, 256);
+    const size_t done_off = round_up(stat_off + sizeof(int) * ispc, 256);
+    for (int si = 0; si < islots; ++si) {
+      int rc = prep_inplace(L.slot[si], tp, done_off + 256);
+      if (rc) return rc;
+      L.slot[si].pending = false;
     }
-    if (sl.small_tables != tp) {
-      // per launch group: [v_perm tables][idx: 256 input + 16 row shard indices]
-      std::vector<size_t> off;
-      size_t tot = 0;
-      for (const Group& g : t.groups) {
-        off.push_back(tot);
-        tot = round_up(tot + g.tabs.size() * sizeof(uint32_t) + 272, 256);
-      }
-      sl.small_tables = nullptr;
-      if ((rc = sl.small_tabs.ensure(tot))) return rc;
-      std::vector<uint8_t> h(tot, 0);
-      for (size_t gi = 0; gi < t.groups.size(); ++gi) {
-        const Group& g = t.groups[gi];
-        const size_t tb = g.tabs.size() * sizeof(uint32_t);
-        std::memcpy(h.data() + off[gi], g.tabs.data(), tb);
-        uint8_t* ix = h.data() + off[gi] + tb;
-        for (int i = 0; i < t.k; ++i) ix[i] = static_cast<uint8_t>(t.valid[i]);
-        for (size_t r = 0; r < g.shard.size(); ++r) ix[256 + r] = static_cast<uint8_t>(g.shard[r]);
-      }
-      HIPCHK(hipMemcpy(sl.small_tabs.p, h.data(), tot, hipMemcpyHostToDevice));
-      sl.small_tables = tp;
-      sl.small_tab_off = off;
-    }
-    auto* base = static_cast<uint8_t*>(sl.small.p);
-    int* st = reinterpret_cast<int*>(base + stat_off);
-    int* done = reinterpret_cast<int*>(base + done_off);
-    const int seq = ++sl.small_seq == 0 ? ++sl.small_seq : sl.small_seq;
-    // a fresh or moved buffer holds whatever it held: clear the flag before the launch
-    __atomic_store_n(done, 0, __ATOMIC_RELEASE);
-    std::vector<CopyPool::Seg> segs;
-    for (int b = 0; b < batch; ++b)
-      for (int i : ins) {
-        const auto tee = join_span(join, i, col0, S);
-        segs.push_back({base + sp16 * b + cp16 * i, host_in(b, i), S, tee.first, tee.second});
-      }
-    ctx->pool.run(segs);
-    if (verify) std::memset(st, 0, sizeof(int) * batch);
-    for (size_t gi = 0; gi < t.groups.size(); ++gi) {
-      const Group& g = t.groups[gi];
-      SmallArgs A{};
-      A.base = base;
-      A.spitch = sp16;
-      A.cpitch = cp16;
-      A.nvec = static_cast<uint32_t>(cp16 / 16);
-      A.S = static_cast<uint32_t>(S);
-      A.K = t.k;
-      A.R = static_cast<int>(g.shard.size());
-      A.batch = batch;
-      A.verify_mask = g.verify_mask;
-      const uint8_t* tb = static_cast<uint8_t*>(sl.small_tabs.p) + sl.small_tab_off[gi];
-      A.tabs = reinterpret_cast<const uint32_t*>(tb);
-      A.idx = tb + g.tabs.size() * sizeof(uint32_t);
-      for (int i = 0; i < std::min(t.k, 16); ++i)
-        A.idx_in[i >> 2] |= static_cast<uint32_t>(t.valid[i]) << (8 * (i & 3));
-      for (size_t r = 0; r < g.shard.size(); ++r)
-        A.idx_out[r >> 2] |= static_cast<uint32_t>(g.shard[r]) << (8 * (r & 3));
-      A.status = st;
-      const bool last = gi + 1 == t.groups.size();
-      A.done = last ? done : nullptr;
-      A.counter = static_cast<unsigned*>(sl.small_counter.p);
-      A.seq = seq;
-      HIPCHK(launch_small(A, sl.stream));
-    }
-    // spin on the kernel's completion flag (~5 us sooner than the runtime's signal); past
-    // kSmallSpinUs, or if the launch failed, fall back to the stream wait, which also
-    // reports a faulted kernel
-    if (!spin_until(done, seq, kSmallSpinUs)) HIPCHK(hipStreamSynchronize(sl.stream));
     bool corrupt = false;
-    if (verify)
-      for (int b = 0; b < batch; ++b)
-        if (st[b]) {
-          corrupt = true;
-          if (stripe_status) stripe_status[b] = 1;
-        }
-    segs.clear();
-    for (int b = 0; b < batch; ++b)
-      for (int i : outs) {
-        const auto tee = join_span(join, i, col0, S);
-        segs.push_back({host_out(b, i), base + sp16 * b + cp16 * i, S, tee.first, tee.second});
+    std::vector<CopyPool::Seg> segs;
+    // waits for the slot's chunk and appends its output copies to `segs`
+    auto drain = [&](Slot& sl) -> int {
+      if (!sl.pending) return RS_OK;
+      auto* base = static_cast<uint8_t*>(sl.small.p);
+      const int* done = reinterpret_cast<const int*>(base + done_off);
+      // ~5 us sooner than the runtime's completion signal; past kSmallSpinUs the stream
+      // wait, which also reports a faulted kernel
+      if (!spin_until(done, sl.small_seq, kSmallSpinUs)) HIPCHK(hipStreamSynchronize(sl.stream));
+      if (verify) {
+        const int* st = reinterpret_cast<const int*>(base + stat_off);
+        for (int b = 0; b < sl.count; ++b)
+          if (st[b]) {
+            corrupt = true;
+            if (stripe_status) stripe_status[sl.b0 + b] = 1;
+          }
       }
-    ctx->pool.run(segs);
+      for (int b = 0; b < sl.count; ++b)
+        for (int i : outs) {
+          const auto tee = join_span(join, i, col0 + sl.off, sl.width);
+          segs.push_back({host_out(sl.b0 + b, i) + sl.off, base + isp * b + icp * i, sl.width,
+                          tee.first, tee.second});
+        }
+      sl.pending = false;
+      return RS_OK;
+    };
+    for (size_t j = 0; j < ichunks; ++j) {
+      Slot& sl = L.slot[j % islots];
+      segs.clear();
+      int rc = drain(sl);
+      if (rc) return rc;
+      const int b0 = static_cast<int>(j / incol) * ispc;
+      const int cnt = std::min(ispc, batch - b0);
+      const size_t off = (j % incol) * icw, w = std::min(icw, S - off);
+      auto* base = static_cast<uint8_t*>(sl.small.p);
+      for (int b = 0; b < cnt; ++b)
+        for (int i : ins) {
+          const auto tee = join_span(join, i, col0 + off, w);
+          segs.push_back({base + isp * b + icp * i, host_in(b0 + b, i) + off, w, tee.first,
+                          tee.second});
+        }
+      ctx->pool.run(segs);
+      int* st = reinterpret_cast<int*>(base + stat_off);
+      int* done = reinterpret_cast<int*>(base + done_off);
+      sl.small_seq = sl.small_seq >= 0x3fffffff ? 1 : sl.small_seq + 1;  // never 0
+      // a fresh or moved buffer holds whatever it held: clear the flag before the launch
+      __atomic_store_n(done, 0, __ATOMIC_RELEASE);
+      if (verify) std::memset(st, 0, sizeof(int) * cnt);
+      HIPCHK(launch_inplace(sl, t, base, isp, icp, w, cnt, st, done, sl.small_seq));
+      sl.pending = true;
+      sl.b0 = b0;
+      sl.count = cnt;
+      sl.off = off;
+      sl.width = w;
+    }
+    for (size_t j = ichunks > static_cast<size_t>(islots) ? ichunks - islots : 0; j < ichunks; ++j) {
+      segs.clear();
+      int rc = drain(L.slot[j % islots]);
+      if (rc) return rc;
+      ctx->pool.run(segs);
+    }
     return corrupt ? RS_E_CORRUPT : RS_OK;
   }
 
