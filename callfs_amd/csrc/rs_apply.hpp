@@ -109,9 +109,7 @@ struct Policy {
   static constexpr int VPF = VPF_;
   static_assert(VPF_ == 0 || (REALIGN_ == 0 && RING_ == 0), "VPF: plain ring-of-three kernel only");
   // tools/kbench layout probes (never dispatched): 1 = 63-vector waves (the REALIGN
-  // tiling) with plain loads, lane 63 idle; 2 = 64-vector waves, lane 63 idle;
-  // epilogue probes (CALLFS_RS_PROBE, R = 4 A/B): 3 = block barrier before the stores of a
-  // full tile (a block's stores leave together), 4 = raised wave priority while storing
+  // tiling) with plain loads, lane 63 idle; 2 = 64-vector waves, lane 63 idle
   static constexpr int PROBE = PROBE_;
   static constexpr bool NOMATH = NOMATH_;
   // LDS table addresses by v_or_b32_sdwa (byte select + OR) instead of v_perm_b32
@@ -764,11 +762,6 @@ void rs_apply_lds(ApplyArgs a) {
     }
 
     bool bad = false;
-    if constexpr (P::PROBE == 3) {
-      // block-uniform: every wave of a full tile is active (none took the `continue`)
-      if ((static_cast<uint64_t>(tile) + 1) * TV <= a.nvec) __syncthreads();
-    }
-    if constexpr (P::PROBE == 4) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       if (r >= R) continue;  // wave-uniform
@@ -802,7 +795,6 @@ void rs_apply_lds(ApplyArgs a) {
         store16<P>(dst, o);
       }
     }
-    if constexpr (P::PROBE == 4) __builtin_amdgcn_s_setprio(0);
     if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
   }
 }

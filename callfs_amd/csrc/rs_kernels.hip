@@ -196,21 +196,6 @@ constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1>>...};
 }
 const auto kLdsRealignOut = lds_realign_out_table(std::make_integer_sequence<int, 8>{});
-// epilogue probes for the bench shape (R = 4, encode-type launches; CALLFS_RS_PROBE=3|4,
-// A/B only): [probe - 3][consecutive, G2]
-const VecFn kLdsProbe[2][2] = {
-    {&dev::rs_apply_lds<4, dev::Policy<2, 1, true, true, false, 512, 2, 0, 0, false, 0, false, 3>>,
-     &dev::rs_apply_lds<4, dev::Policy<2, 1, true, true, false, 512, 2, 5, 0, false, 0, false, 3>>},
-    {&dev::rs_apply_lds<4, dev::Policy<2, 1, true, true, false, 512, 2, 0, 0, false, 0, false, 4>>,
-     &dev::rs_apply_lds<4, dev::Policy<2, 1, true, true, false, 512, 2, 5, 0, false, 0, false, 4>>}};
-int epilogue_probe() {
-  static const int v = [] {
-    const char* e = std::getenv("CALLFS_RS_PROBE");
-    const int x = e ? std::atoi(e) : 0;
-    return x == 3 || x == 4 ? x : 0;
-  }();
-  return v;
-}
 template <class P, int... Rs>
 constexpr auto lds_wide_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 9, P>...};
@@ -376,9 +361,6 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           const uint32_t rows = (1u << a.R) - 1;
           const int oi = static_cast<int>(ord);
           if (a.R <= 4 && (a.verify_mask & rows) && oi >= 0 && oi < 5) fn = kLdsVerify[oi][a.R - 1];
-          if (a.R == 4 && !(a.verify_mask & rows) && epilogue_probe() &&
-              (ord == TileOrder::kConsecutive || ord == TileOrder::kGroup2))
-            fn = kLdsProbe[epilogue_probe() - 3][ord == TileOrder::kGroup2];
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }
