@@ -58,8 +58,9 @@ inline int split_ways_request(const char* env) {
 }
 
 // One-time setup per (device, key), e.g. the > 64 KiB dynamic-LDS opt-in of the wide
-// kernels: hipFuncSetAttribute applies to the calling thread's current device only, so
-// a once-flag per kernel would leave every device but the first without it. `run`
+// kernels (launch_apply, key R - 9): hipFuncSetAttribute applies to the calling thread's
+// current device only, so a once-flag per kernel would leave every device but the first
+// without it. `run`
 // calls f() the first time a (device, key) pair is seen and returns whether it did;
 // concurrent callers of one pair wait until f() has returned. Devices outside
 // [0, kMaxDevices) and keys outside [0, 64) run f() every time.
@@ -88,18 +89,6 @@ class DeviceOnce {
   std::atomic<uint64_t> done_[kMaxDevices] = {};
   std::mutex mu_;
 };
-
-// rs_init: per-device setup of every selected device (make it current, then run `setup`
-// for each key); returns false at the first device that cannot be made current.
-template <class SetDevice, class Setup>
-bool setup_devices(const std::vector<int>& devs, DeviceOnce& once, int nkeys,
-                   SetDevice&& set_device, Setup&& setup) {
-  for (int d : devs) {
-    if (!set_device(d)) return false;
-    for (int key = 0; key < nkeys; ++key) once.run(d, key, [&] { setup(d, key); });
-  }
-  return true;
-}
 
 // Column boundaries c[0..ways] of an S-byte shard: c[0] = 0, c[ways] = S, interior
 // boundaries 4 KiB aligned (parts may be empty only when S is tiny).

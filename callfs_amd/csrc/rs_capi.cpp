@@ -1234,14 +1234,9 @@ int rs_init(rs_ctx** out, unsigned device_mask) {
     ctx->devs.push_back(std::move(dev));
   }
   if (ctx->devs.empty()) return RS_E_HIP;
-  // the wide kernels' > 64 KiB dynamic-LDS opt-in, on every selected device (it is a
-  // per-device attribute; launch_apply repeats it on first use for other devices)
-  {
-    DeviceGuard dg;
-    std::vector<int> ids;
-    for (auto& d : ctx->devs) ids.push_back(d->id);
-    if (!callfs::prepare_devices(ids)) return RS_E_HIP;
-  }
+  // (the wide kernels' > 64 KiB dynamic-LDS opt-in is a per-device attribute: launch_apply
+  // issues it once per (device, R) before the first such launch on a device, so rs_init
+  // touches no device -- a process per GPU must not load code onto all eight)
   *out = ctx.release();
   return RS_OK;
 }

@@ -208,7 +208,6 @@ const auto kByte = byte_table(std::make_integer_sequence<int, kMaxRowsPerLaunch>
 // (device, R), key R - 9 (dispatch.hpp DeviceOnce). Both tile-order instances of an R
 // opt in together.
 DeviceOnce g_wide_lds;
-constexpr int kWideKeys = kMaxRowsPerLaunch - 8;
 
 void wide_lds_opt_in(int R) {
   for (VecFn f : {kLds[R - 1], kLdsWideQ8[R - 9]})
@@ -237,15 +236,6 @@ hipError_t launch_small(const SmallArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-bool prepare_devices(const std::vector<int>& devices) {
-  return setup_devices(
-      devices, g_wide_lds, kWideKeys, [](int d) { return hipSetDevice(d) == hipSuccess; },
-      [](int, int key) { wide_lds_opt_in(key + 9); });
-}
-
-bool wide_lds_ready(int device, int R) {
-  return R >= 9 && R <= kMaxRowsPerLaunch && g_wide_lds.done(device, R - 9);
-}
 
 void set_slice_tiles_for_tuning(long long tiles) {
   g_slice_tiles_override.store(tiles, std::memory_order_relaxed);
@@ -365,8 +355,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           fn = kLdsWideQ8[a.R - 9];
         }
         if (lds > (64u << 10)) {  // wide groups with many shards (only R > 8 gets here):
-          // the opt-in is per device; rs_init issued it for the context's devices, this
-          // covers plans and device calls on any other device
+          // the opt-in is a per-device attribute: once per (device, R), before the first
+          // such launch on each device (a once-flag per kernel left devices 1..7 without it)
           int device = -1;
           if (hipGetDevice(&device) != hipSuccess) return hipErrorInvalidDevice;
           g_wide_lds.run(device, a.R - 9, [&a] { wide_lds_opt_in(a.R); });

@@ -124,12 +124,6 @@ std::vector<int> order_candidates(const ApplyArgs& a);
 //   mode 2  its write streams alone (junk into the written rows).
 hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode);
 
-// rs_init: per-device setup of the kernels for each listed device (the > 64 KiB
-// dynamic-LDS opt-in of the 9..16-row instances, a per-device attribute); leaves the
-// last listed device current. launch_apply also issues it on first use per device.
-bool prepare_devices(const std::vector<int>& devices);
-// whether the opt-in for R rows (9..16) has been issued on `device` (tests)
-bool wide_lds_ready(int device, int R);
 
 // Tuning hook for tools/kbench.hip (not part of the C ABI): tiles per launch slice for
 // every later launch_apply in the process; 0 = never slice, < 0 = the built-in rule

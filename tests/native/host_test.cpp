@@ -9,8 +9,8 @@
 //     the launch rules pick the measured orders for known layouts
 //  6. multi-device placement (dispatch.hpp) over mocked device lists: mask selection,
 //     round-robin device slots, split ways and column part boundaries
-//  7. per-device kernel setup (DeviceOnce / setup_devices): the wide kernels' dynamic-LDS
-//     opt-in is issued on every selected device, once per (device, R)
+//  7. per-device kernel setup (DeviceOnce): the wide kernels' dynamic-LDS opt-in is issued
+//     once per (device, R), before the first such launch on each device
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -321,41 +321,38 @@ int main() {
     CHECK(split_ways(8, 8, S1g, 14, 1, min_b, split_ways_request(nullptr)) == 8);
   }
   // 7. per-device kernel setup (the wide kernels' > 64 KiB dynamic-LDS opt-in is a
-  // per-device attribute): rs_init issues it on every selected device, once per
-  // (device, R); a launch on any device, selected or not, finds it issued or issues it
-  // first; concurrent first launches issue it once
+  // per-device attribute): launch_apply issues it once per (device, R) before the first
+  // such launch on a device -- every device of a mocked 8-device context gets it before its
+  // first launch whatever the launch order, exactly once, with the device current; other
+  // keys and devices stay untouched; concurrent first launches issue it once
   {
     for (unsigned mask : {0u, 0x81u, 0x0Eu}) {
       DeviceOnce once;
       const std::vector<int> devs = select_devices(8, mask);
-      int current = -1;
       std::vector<std::vector<int>> issued(8, std::vector<int>(8, 0));  // [device][R - 9]
-      CHECK(setup_devices(devs, once, 8, [&](int d) { current = d; return true; },
-                          [&](int d, int key) {
-                            CHECK(d == current);  // issued with that device current
-                            issued[d][key]++;
-                          }));
+      int current = -1;
+      auto launch = [&](int d, int R) {  // what launch_apply does for a wide launch on d
+        current = d;
+        once.run(d, R - 9, [&] {
+          CHECK(current == d);
+          issued[d][R - 9]++;
+        });
+        CHECK(once.done(d, R - 9));  // issued before the launch proceeds
+      };
+      for (int rep = 0; rep < 3; ++rep)
+        for (size_t j = 0; j < devs.size(); ++j) {
+          const int d = devs[(j * 5 + rep) % devs.size()];  // scrambled device order
+          for (int R : {16, 9, 12}) launch(d, R);
+        }
       for (int d = 0; d < 8; ++d) {
         const bool sel = std::find(devs.begin(), devs.end(), d) != devs.end();
-        for (int key = 0; key < 8; ++key) {
-          CHECK(issued[d][key] == (sel ? 1 : 0));
-          CHECK(once.done(d, key) == sel);
+        for (int R = 9; R <= 16; ++R) {
+          const bool used = sel && (R == 16 || R == 9 || R == 12);
+          CHECK(issued[d][R - 9] == (used ? 1 : 0));
+          CHECK(once.done(d, R - 9) == used);
         }
       }
-      // launches on every device in a scrambled order: each (device, R) issued exactly
-      // once overall, before the launch proceeds
-      for (int rep = 0; rep < 3; ++rep)
-        for (int d : {5, 0, 7, 3, 1, 6, 2, 4})
-          for (int key : {7, 0, 3}) {
-            once.run(d, key, [&] { issued[d][key]++; });
-            CHECK(once.done(d, key));
-          }
-      for (int d = 0; d < 8; ++d)
-        for (int key : {7, 0, 3}) CHECK(issued[d][key] == 1);
     }
-    // a failing set_device stops rs_init
-    DeviceOnce once;
-    CHECK(!setup_devices({0, 1}, once, 8, [](int d) { return d == 0; }, [](int, int) {}));
     // concurrent first use of one (device, key): one call
     DeviceOnce once2;
     std::atomic<int> calls{0};
@@ -366,6 +363,12 @@ int main() {
       });
     for (auto& t : th) t.join();
     CHECK(calls.load() == 8);
+    // out-of-range devices / keys run every time (never silently skipped)
+    int n = 0;
+    once2.run(40, 0, [&] { n++; });
+    once2.run(40, 0, [&] { n++; });
+    once2.run(0, 70, [&] { n++; });
+    CHECK(n == 3);
   }
   std::printf(fails ? "FAILED %d\n" : "host_test ok\n", fails);
   return fails ? 1 : 0;
