@@ -83,6 +83,7 @@ SIGNATURES = {
     "rs_plan_launch_ceiling": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "rs_plan_destroy": (None, [_vp]),
     "rs_plan_tune": (_int, [_vp, _vp, _int, ctypes.POINTER(_int), _int]),
+    "rs_plan_set_orders": (_int, [_vp, ctypes.POINTER(_int), _int]),
     "rs_encode_dev": (_int, [_vp, _int, _int, _int, _sz, _int, ctypes.POINTER(_vp), _vp]),
     "rs_decode_dev": (_int, [_vp, _int, _int, _int, _sz, _int, _u8p, ctypes.POINTER(_vp), _vp]),
     "rs_sha256_plan_create": (_int, [_vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64),

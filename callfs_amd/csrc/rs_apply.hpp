@@ -90,7 +90,9 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //   BS       threads per block; PD prefetch depth in input-shard pairs (1 or 2)
 //   ORD      tile order: 0 = a stripe's tiles consecutive, 1 = interleaved across all
 //            stripes, 2/3/4/5 = interleaved within groups of 8/32/4/2 stripes, 6/7/8/9 =
-//            interleaved across 8/32/16/64 column segments of one stripe (LDS kernel: 0, 2..9)
+//            interleaved across 8/32/16/64 column segments of one stripe, 10/11 = consecutive
+//            with J = 8/32 consecutive tiles per XCD (tile_order.hpp block_tile; LDS kernel:
+//            0, 2..11)
 //   RING     LDS kernel input ring: 0 = three registers shifted each step (PD = 2);
 //            1 = PD+1 slots with the loop unrolled PD+1 times (static slot indices)
 //   NOMATH   measurement only (tools/kbench.hip): the LDS kernel with its lookups
@@ -115,11 +117,17 @@ struct Policy {
   // LDS table addresses by v_or_b32_sdwa (byte select + OR) instead of v_perm_b32
   static constexpr bool SDWA = SDWA_;
   // 0: plain; 1: aligned loads realigned in registers (63 vectors per wave); 2: loads and
-  // parity stores both aligned (62 vectors per wave, edge bytes in the first tile)
+  // parity stores both aligned (62 vectors per wave, edge bytes in the first tile);
+  // 4: REALIGN 1's loads, parity stores staged through LDS and written from each row's
+  // first 128-B boundary on (every wave's 1 KiB store 128-B aligned; lds_stage_store)
   static constexpr int REALIGN = REALIGN_;
-  // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads
+  // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads;
+  // REALIGN 4 tiles are 8 vectors shorter than their waves' 8 x 63 results, so that a
+  // row's 128-B-aligned store window, up to 127 bytes past the tile, has its results
   static constexpr int WAVE_VECS = REALIGN_ == 2 ? 62 : (REALIGN_ || PROBE_ == 1) ? 63 : 64;
-  static constexpr int TILE_VECS = WAVE_VECS < 64 ? BS_ / 64 * WAVE_VECS : BS_ * U_;
+  static constexpr int TILE_VECS = REALIGN_ == 4      ? BS_ / 64 * 63 - 8
+                                   : WAVE_VECS < 64 ? BS_ / 64 * WAVE_VECS
+                                                    : BS_ * U_;
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
   static constexpr bool NT_LOAD = NT_LOAD_;
@@ -427,6 +435,14 @@ struct LdsAcc {
 template <class T>
 using lds_ptr = const __attribute__((address_space(3))) T*;
 
+// Dynamic LDS bytes of rs_apply_lds's tables for K input shards and RT rows (REALIGN 4
+// adds its staging slots after them: lds_stage_bytes).
+__host__ __device__ inline size_t lds_bytes(int K, int RT) {
+  return static_cast<size_t>(K) * 32 * (RT > 8 ? 16 : 8);
+}
+constexpr int kStageRows = 4;  // REALIGN 4: rows staged per block barrier
+inline size_t lds_stage_bytes(int BS) { return static_cast<size_t>(kStageRows) * (BS / 64 * 63) * 16; }
+
 // One table entry at an absolute 32-bit LDS address (no base add per lookup).
 template <int RT>
 __device__ __forceinline__ typename LdsAcc<RT>::T lds_lookup(uint32_t addr) {
@@ -637,6 +653,73 @@ __device__ __forceinline__ void lds_edges(const ApplyArgs& a, cptr<const uint8_t
   if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
 }
 
+// ---- parity stores from 128-B boundaries (Policy::REALIGN == 4) ------------------------
+// A wave-instruction's 1 KiB store that starts off a 128-B boundary writes at 60-64 % of
+// spec alone, from a 128-B boundary at 74-75 % (tools/write_align_probe.py, Split layout
+// and 16-B pitches). The rows of a stripe sit at different offsets mod 128, so no tiling
+// of the vectors aligns them all: each written row r is staged through LDS and stored
+// from h_r = (-q_r) & 127 on (q_r = the row's address). A tile of TV = 496 vectors at T0
+// (TV a multiple of 8: the same h_r in every tile) stores the 496 16-B blocks at shard
+// bytes 16 T0 + h_r + 16 j, j < 496, and block j needs results T0 + (h_r >> 4) + j and the
+// next: up to T0 + 503, which its 8 waves x 63 results cover. Thread j reads the two
+// 16-B slots from LDS and funnel-shifts them by h_r & 15. Blocks past the row's last
+// full vector are not stored; lds_edges128 writes the head [0, h_r) and that tail.
+template <int BS>
+constexpr int stage_slots() { return BS / 64 * 63; }
+// bytes [sh, sh + 16) of A:B (sh in 0..15)
+__device__ __forceinline__ uint4 funnel_bytes(const uint4& A, const uint4& B, uint32_t sh) {
+  const uint32_t r = sh & 3u;
+  switch (sh >> 2) {
+    case 0: return funnel16<0>(A, B, r);
+    case 1: return funnel16<1>(A, B, r);
+    case 2: return funnel16<2>(A, B, r);
+    default: return funnel16<3>(A, B, r);
+  }
+}
+
+// Edge bytes of a REALIGN == 4 launch, one byte position per thread: threads 0..127 take
+// bytes 0..127, threads 128..159 the bytes from max(128, 16 nvec - 16) on (< 32 of them:
+// S < 16 nvec + 16). Written row r owns [0, h_r) and [E_r, S), E_r = the end of its last
+// stored block; Verify rows own [16 nvec, S) (their vectors are compared in place).
+template <int RT>
+__device__ __forceinline__ void lds_edges128(const ApplyArgs& a, cptr<const uint8_t*> in,
+                                             cptr<uint8_t*> out, uint32_t stripe, uint32_t lds0) {
+  constexpr int W = LdsAcc<RT>::W;
+  const uint32_t j = threadIdx.x;
+  if (j >= 160u) return;
+  const uint64_t full = a.nvec * 16;  // nvec >= 1 on this path
+  const uint64_t tb = full - 16 > 128 ? full - 16 : 128;
+  const uint64_t b = j < 128u ? j : tb + (j - 128u);
+  if (b >= a.S) return;
+  typename LdsAcc<RT>::T t = lds_zero<RT>();
+  for (int i0 = 0; i0 < a.K; i0 += tail_loads<RT>()) {
+    uint32_t x[tail_loads<RT>()];
+    tail_bytes<RT>(in, b, i0, a.K, x);
+    for (int jj = 0; jj < tail_loads<RT>() && i0 + jj < a.K; ++jj) {
+      const uint32_t base = lds0 + static_cast<uint32_t>(i0 + jj) * 32u * W;
+      t = t ^ lds_lookup<RT>(base + (x[jj] & 15u) * W) ^
+          lds_lookup<RT>(base + 16u * W + (x[jj] >> 4) * W);
+    }
+  }
+  bool bad = false;
+  for (int r = 0; r < a.R && r < RT; ++r) {
+    const uint8_t v = static_cast<uint8_t>(lds_byte<RT>(t, r));
+    const bool verify = (a.verify_mask >> r) & 1u;
+    bool mine;
+    if (verify) {
+      mine = b >= full;
+    } else {
+      const uint64_t h = (0u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r]))) & 127u;
+      const uint64_t e = full >= h ? h + ((full - h) & ~uint64_t(15)) : h;
+      mine = b < h || b >= e;
+    }
+    if (!mine) continue;
+    if (verify) bad |= out[r][b] != v;
+    else out[r][b] = v;
+  }
+  if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
+}
+
 // Waves per SIMD the LDS kernel may be limited to: 16-byte entries keep 8 b128 reads
 // (32 VGPRs) in flight, which the register allocator only grants below 5 waves.
 template <int RT>
@@ -668,7 +751,8 @@ void rs_apply_lds(ApplyArgs a) {
   // one tile per block (vec_grid), or (PERSIST) grid-stride over tiles so that the
   // table prologue is paid once per block; either way the blocks in flight cover a
   // window of consecutive t, which is what the tile order arranges
-  for (uint32_t t = a.t_base + blockIdx.x; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
+  const uint32_t t0 = a.t_base + (P::PERSIST ? blockIdx.x : block_tile<P::ORD>(blockIdx.x, gridDim.x));
+  for (uint32_t t = t0; t < ntiles; t += (P::PERSIST ? gridDim.x : ntiles)) {
     uint32_t stripe, tile;
     map_tile<P::ORD>(t, tps, static_cast<uint32_t>(a.batch), stripe, tile);
     // REALIGN: wave w of the tile produces vectors tile*TV + 63w + lane (lanes 0..62)
@@ -678,7 +762,9 @@ void rs_apply_lds(ApplyArgs a) {
                                 : static_cast<uint64_t>(tile) * BS + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
-    if constexpr (P::REALIGN == 2) {
+    if constexpr (P::REALIGN == 4) {
+      if (tile == 0) lds_edges128<RT>(a, in, out, stripe, lds0);
+    } else if constexpr (P::REALIGN == 2) {
       if (tile == 0) lds_edges<RT>(a, in, out, stripe, lds0);
     } else {
       if (tile == 0 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
@@ -686,7 +772,9 @@ void rs_apply_lds(ApplyArgs a) {
     // lanes that store (REALIGN: lane 63 -- REALIGN 2: lanes 62, 63 -- and lanes past the
     // shard only load)
     const bool active = v0 < a.nvec && lane < WV && !(P::PROBE == 2 && lane == 63u);
-    if (P::REALIGN ? (v0 - lane >= a.nvec) : !active) continue;  // REALIGN: whole wave idle
+    // REALIGN: whole wave idle (REALIGN 4 never leaves: its waves meet at block barriers;
+    // an idle wave's loads are clamped into the shard and its results never stored)
+    if (P::REALIGN != 4 && (P::REALIGN ? (v0 - lane >= a.nvec) : !active)) continue;
     auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
     AccT acc[4][4];
 #pragma unroll
@@ -768,6 +856,9 @@ void rs_apply_lds(ApplyArgs a) {
       const uint4 o = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
                                  lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
       uint4* dst = reinterpret_cast<uint4*>(out[r]) + v0;
+      if constexpr (P::REALIGN == 4) {
+        if (!((a.verify_mask >> r) & 1u)) continue;  // written rows: staged below
+      }
       if constexpr (P::REALIGN == 2) {
         if (!((a.verify_mask >> r) & 1u)) {
           const uint32_t mo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r])) & 15u;
@@ -796,6 +887,49 @@ void rs_apply_lds(ApplyArgs a) {
       }
     }
     if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
+    if constexpr (P::REALIGN == 4) {
+      // written rows through LDS, kStageRows per barrier (block-uniform branches: R and
+      // verify_mask are kernel arguments)
+      constexpr int NS = stage_slots<BS>();
+      static_assert(TV % 8 == 0 && TV + 8 <= NS, "128-B windows need 8 spare results");
+      const uint32_t st0 = lds0 + static_cast<uint32_t>(lds_bytes(K, RT));
+      const uint32_t wave = threadIdx.x >> 6;
+#pragma unroll
+      for (int r0 = 0; r0 < RT; r0 += kStageRows) {
+        if (r0 >= R) break;
+        if (r0 > 0) __syncthreads();  // the previous rows' slots have been read
+#pragma unroll
+        for (int c = 0; c < kStageRows; ++c) {
+          const int r = r0 + c;
+          if (r >= RT || r >= R || ((a.verify_mask >> r) & 1u)) continue;
+          const uint4 o = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
+                                     lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
+          if (lane < 63u) {
+            const uint32_t ad = st0 + (static_cast<uint32_t>(c) * NS + wave * 63u + lane) * 16u;
+            *(__attribute__((address_space(3))) u32x4*)(static_cast<uintptr_t>(ad)) =
+                u32x4{o.x, o.y, o.z, o.w};
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < kStageRows; ++c) {
+          const int r = r0 + c;
+          if (r >= RT || r >= R || ((a.verify_mask >> r) & 1u)) continue;
+          const uint32_t h = (0u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r]))) & 127u;
+          const uint32_t j = threadIdx.x;
+          const uint64_t p = (static_cast<uint64_t>(tile) * TV + j) * 16u + h;  // shard byte
+          if (j >= static_cast<uint32_t>(TV) || p + 16 > a.nvec * 16) continue;
+          const uint32_t ad = st0 + (static_cast<uint32_t>(c) * NS + (h >> 4) + j) * 16u;
+          const u32x4 A = *(lds_ptr<u32x4>)(static_cast<uintptr_t>(ad));
+          uint4 X = make_uint4(A.x, A.y, A.z, A.w);
+          if (h & 15u) {
+            const u32x4 B = *(lds_ptr<u32x4>)(static_cast<uintptr_t>(ad + 16u));
+            X = funnel_bytes(X, make_uint4(B.x, B.y, B.z, B.w), h & 15u);
+          }
+          store16<P>(reinterpret_cast<uint4*>(out[r] + p), X);  // 16-B (128-B per wave) aligned
+        }
+      }
+    }
   }
 }
 
@@ -819,7 +953,8 @@ template <int ORD>
 __global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
   const uint32_t tps = static_cast<uint32_t>((a.nvec + 511) / 512);
   uint32_t stripe, tile;
-  map_tile<ORD>(a.t_base + blockIdx.x, tps, static_cast<uint32_t>(a.batch), stripe, tile);
+  map_tile<ORD>(a.t_base + block_tile<ORD>(blockIdx.x, gridDim.x), tps,
+                static_cast<uint32_t>(a.batch), stripe, tile);
   const uint64_t v0 = static_cast<uint64_t>(tile) * 512 + threadIdx.x;
   if (v0 >= a.nvec) return;
   cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * a.K;
@@ -853,11 +988,14 @@ __global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
     a.status[0] = static_cast<int>(v0);
 }
 
-template <int ORD>
+// AL > 16 (measurement probe): each row is written from its first AL-byte boundary on, so
+// every wave-instruction's 1 KiB store starts on an AL-byte boundary
+template <int ORD, int AL = 16>
 __global__ __launch_bounds__(512) void rs_stream_write(ApplyArgs a) {
   const uint32_t tps = static_cast<uint32_t>((a.nvec + 511) / 512);
   uint32_t stripe, tile;
-  map_tile<ORD>(a.t_base + blockIdx.x, tps, static_cast<uint32_t>(a.batch), stripe, tile);
+  map_tile<ORD>(a.t_base + block_tile<ORD>(blockIdx.x, gridDim.x), tps,
+                static_cast<uint32_t>(a.batch), stripe, tile);
   const uint64_t v0 = static_cast<uint64_t>(tile) * 512 + threadIdx.x;
   if (v0 >= a.nvec) return;
   cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * a.R;
@@ -868,14 +1006,12 @@ __global__ __launch_bounds__(512) void rs_stream_write(ApplyArgs a) {
       // aligned blocks inside the row: from the first 16-B boundary at or after its base,
       // one block fewer when the base is misaligned (never a byte outside [base, base + S))
       const uintptr_t q = reinterpret_cast<uintptr_t>(out[r]);
-      const uintptr_t up = (q + 15) & ~uintptr_t(15);
-      if (up != q && v0 + 1 >= a.nvec) continue;
+      const uintptr_t up = (q + AL - 1) & ~uintptr_t(AL - 1);
+      if (up + 16 * (v0 + 1) > q + a.S) continue;
       store16<P>(reinterpret_cast<uint4*>(up) + v0, make_uint4(x, x + 1, x + 2, x + r));
     }
 }
 
-// Dynamic LDS bytes of rs_apply_lds for K input shards and RT rows.
-inline size_t lds_bytes(int K, int RT) { return static_cast<size_t>(K) * 32 * (RT > 8 ? 16 : 8); }
 
 // One byte position per lane over [b0, S): ragged tails (S % 16).
 template <int RT>

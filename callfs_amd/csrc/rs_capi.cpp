@@ -1604,7 +1604,7 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
 
 int rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode) {
   DeviceGuard dg;
-  if (!plan || mode < 0 || mode > 2) return RS_E_ARG;
+  if (!plan || mode < 0 || mode > 5) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
   std::vector<int> orders;
   {
@@ -1735,6 +1735,28 @@ int rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_gro
   }
   for (int i = 0; i < max_groups; ++i)
     orders[i] = static_cast<size_t>(i) < chosen.size() ? chosen[i] : -1;
+  return RS_OK;
+}
+
+// Pins launch group i to orders[i] (-1: the rule), as rs_plan_tune would: the order must
+// be one order_candidates offers for that group's kernel (RS_E_ARG otherwise, and nothing
+// changes). For orders tuned once and kept (a deployment's own shard layout), and for
+// tests that run every instance.
+int rs_plan_set_orders(rs_plan* plan, const int* orders, int n) {
+  if (!plan || n < 0 || (n > 0 && !orders)) return RS_E_ARG;
+  const Tables& t = *plan->tables;
+  if (static_cast<size_t>(n) > t.groups.size()) return RS_E_ARG;
+  auto* d = static_cast<uint8_t*>(plan->dmeta);
+  std::vector<int> next(t.groups.size(), -1);
+  for (int gi = 0; gi < n; ++gi) {
+    if (orders[gi] == -1) continue;
+    const ApplyArgs a = group_args(t, plan->layout, gi, plan->batch, d, plan->S, 1, plan->hint);
+    const std::vector<int> cand = order_candidates(a);
+    if (std::find(cand.begin(), cand.end(), orders[gi]) == cand.end()) return RS_E_ARG;
+    next[gi] = orders[gi];
+  }
+  std::lock_guard<std::mutex> g(plan->mu);
+  plan->orders = next;
   return RS_OK;
 }
 

@@ -57,6 +57,8 @@ using LdsG8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 2>;
 using LdsG2Policy = dev::Policy<2, 1, true, true, false, 512, 2, 5>;
 using LdsQ8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 6>;
 using LdsQ16Policy = dev::Policy<2, 1, true, true, false, 512, 2, 8>;
+using LdsX8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 10>;
+using LdsX32Policy = dev::Policy<2, 1, true, true, false, 512, 2, 11>;
 // Launch groups of R <= 4 rows with Verify rows load the compared vectors 4 shards before
 // the end of the input loop (rs_apply.hpp Policy::VPF): tools/verify_prefetch_probe.sh,
 // profiles/r02/verify_prefetch/, RS(10,4) 1 MiB x 256, % of 8 TB/s, after the loop ->
@@ -78,12 +80,19 @@ using LdsVerifyPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, fal
 // -> 72.2, RS(4,2) 69.0 -> 69.1 -> 69.8; RS(12,4) S = 5,592,406 ran 71.2 unaligned and
 // 68.9 realigned, so rs_plan_tune offers the unaligned kernel as an alternative.
 // (R <= 4 asks for 8 waves per SIMD: left alone the compiler used 106 SGPRs, 7 waves)
-using LdsRealignOutPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0, 0, false, 2>;
-using LdsRealignOut8Policy = dev::Policy<8, 1, true, true, false, 512, 2, 0, 0, false, 2>;
-template <int R>
+// One instance per tile order it runs in: consecutive, X8, X32 (tile_order.hpp block_tile).
+template <int ORD>
+using LdsRealignOutPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 2>;
+template <int ORD>
+using LdsRealignOut8Policy = dev::Policy<8, 1, true, true, false, 512, 2, ORD, 0, false, 2>;
+template <int R, int ORD>
 using LdsRealignOutPolicyFor =
-    typename std::conditional<(R <= 4), LdsRealignOut8Policy, LdsRealignOutPolicy>::type;
-// CALLFS_RS_TILE_ORDER=consecutive|g8|g2|q8|q16 overrides the rule for every LDS-kernel
+    typename std::conditional<(R <= 4), LdsRealignOut8Policy<ORD>, LdsRealignOutPolicy<ORD>>::type;
+// The same loads with the parity stores staged through LDS and written from each row's
+// first 128-B boundary (rs_apply.hpp REALIGN 4).
+template <int R, int ORD>
+using LdsStagePolicyFor = dev::Policy<(R <= 4 ? 8 : 6), 1, true, true, false, 512, 2, ORD, 0, false, 4>;
+// CALLFS_RS_TILE_ORDER=consecutive|g8|g2|q8|q16|x8|x32 overrides the rule for every LDS-kernel
 // launch with R <= 8 (A/B on a deployment's own shard layout; unset = the rule).
 int tile_order_override() {
   static const int v = [] {
@@ -95,6 +104,8 @@ int tile_order_override() {
     if (o == "g2") return static_cast<int>(TileOrder::kGroup2);
     if (o == "q8") return static_cast<int>(TileOrder::kSeg8);
     if (o == "q16") return static_cast<int>(TileOrder::kSeg16);
+    if (o == "x8") return static_cast<int>(TileOrder::kXcd8);
+    if (o == "x32") return static_cast<int>(TileOrder::kXcd32);
     return -1;
   }();
   return v;
@@ -184,18 +195,35 @@ const auto kLdsG8 = lds_order_table<LdsG8Policy>(std::make_integer_sequence<int,
 const auto kLdsG2 = lds_order_table<LdsG2Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ8 = lds_order_table<LdsQ8Policy>(std::make_integer_sequence<int, 8>{});
 const auto kLdsQ16 = lds_order_table<LdsQ16Policy>(std::make_integer_sequence<int, 8>{});
+const auto kLdsX8 = lds_order_table<LdsX8Policy>(std::make_integer_sequence<int, 8>{});
+const auto kLdsX32 = lds_order_table<LdsX32Policy>(std::make_integer_sequence<int, 8>{});
 // [tile order][R - 1] for R <= 4 with Verify rows (TileOrder values index the first level)
-const std::array<std::array<VecFn, 4>, 5> kLdsVerify = {
+const std::array<std::array<VecFn, 4>, kTileOrders> kLdsVerify = {
     lds_order_table<LdsVerifyPolicy<0>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsVerifyPolicy<2>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsVerifyPolicy<5>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsVerifyPolicy<6>>(std::make_integer_sequence<int, 4>{}),
-    lds_order_table<LdsVerifyPolicy<8>>(std::make_integer_sequence<int, 4>{})};
-template <int... Rs>
+    lds_order_table<LdsVerifyPolicy<8>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsVerifyPolicy<10>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsVerifyPolicy<11>>(std::make_integer_sequence<int, 4>{})};
+template <int ORD, int... Rs>
 constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
-  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1>>...};
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1, ORD>>...};
 }
-const auto kLdsRealignOut = lds_realign_out_table(std::make_integer_sequence<int, 8>{});
+template <int ORD, int... Rs>
+constexpr auto lds_stage_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsStagePolicyFor<Rs + 1, ORD>>...};
+}
+// [consecutive, X8, X32][R - 1]
+const std::array<std::array<VecFn, 8>, 3> kLdsStage = {
+    lds_stage_table<0>(std::make_integer_sequence<int, 8>{}),
+    lds_stage_table<10>(std::make_integer_sequence<int, 8>{}),
+    lds_stage_table<11>(std::make_integer_sequence<int, 8>{})};
+// [consecutive, X8, X32][R - 1]
+const std::array<std::array<VecFn, 8>, 3> kLdsRealignOut = {
+    lds_realign_out_table<0>(std::make_integer_sequence<int, 8>{}),
+    lds_realign_out_table<10>(std::make_integer_sequence<int, 8>{}),
+    lds_realign_out_table<11>(std::make_integer_sequence<int, 8>{})};
 template <class P, int... Rs>
 constexpr auto lds_wide_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 9, P>...};
@@ -282,6 +310,22 @@ bool takes_realign(const ApplyArgs& a) {
   return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u);
 }
 
+// The staging form needs its tables and 4 rows of staging slots in the default 64 KiB of
+// dynamic LDS (k <= 130 at R <= 8)
+bool can_stage(const ApplyArgs& a) {
+  return can_realign(a) && dev::lds_bytes(a.K, a.R) + dev::lds_stage_bytes(LdsPolicy::BS) <= (64u << 10);
+}
+
+// The realigning kernel's tile order: consecutive, or X8 / X32 when CALLFS_RS_TILE_ORDER
+// names them; a tuned realign code (kOrderRealign + TileOrder) names it directly.
+// Returns the index into kLdsRealignOut.
+int realign_order_index(int order) {
+  const int o = order >= kOrderStage     ? order - kOrderStage
+                : order >= kOrderRealign ? order - kOrderRealign
+                                         : tile_order_override();
+  return o == static_cast<int>(TileOrder::kXcd8) ? 1 : o == static_cast<int>(TileOrder::kXcd32) ? 2 : 0;
+}
+
 }  // namespace
 
 std::vector<int> order_candidates(const ApplyArgs& a0) {
@@ -303,7 +347,16 @@ std::vector<int> order_candidates(const ApplyArgs& a0) {
     }
     if (takes_realign(a)) add(static_cast<TileOrder>(kOrderRealign));
     add(lds_rule(a));
-    if (can_realign(a)) add(static_cast<TileOrder>(kOrderRealign));
+    if (can_realign(a)) {
+      add(static_cast<TileOrder>(kOrderRealign));
+      add(static_cast<TileOrder>(kOrderRealign + static_cast<int>(TileOrder::kXcd8)));
+      add(static_cast<TileOrder>(kOrderRealign + static_cast<int>(TileOrder::kXcd32)));
+      if (can_stage(a)) {
+        add(static_cast<TileOrder>(kOrderStage));
+        add(static_cast<TileOrder>(kOrderStage + static_cast<int>(TileOrder::kXcd8)));
+        add(static_cast<TileOrder>(kOrderStage + static_cast<int>(TileOrder::kXcd32)));
+      }
+    }
     add(TileOrder::kConsecutive);
     add(TileOrder::kGroup2);
     if (tps <= 32) add(TileOrder::kGroup8);
@@ -311,6 +364,8 @@ std::vector<int> order_candidates(const ApplyArgs& a0) {
       add(TileOrder::kSeg8);
       add(TileOrder::kSeg16);
     }
+    add(TileOrder::kXcd8);
+    add(TileOrder::kXcd32);
     return c;
   }
   add(vec_rule(a));
@@ -336,21 +391,24 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         a.tail_in_vec = tail0 < a.S;
         if (a.tail_in_vec) tail0 = a.S;
         if (!a.ltabs) return hipErrorInvalidValue;
-        const size_t lds = dev::lds_bytes(a.K, a.R);
+        size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
           const TileOrder ord =
-              order >= 0 && order != kOrderRealign ? static_cast<TileOrder>(order) : lds_rule(a);
+              order >= 0 && order < kOrderRealign ? static_cast<TileOrder>(order) : lds_rule(a);
           switch (ord) {
             case TileOrder::kGroup8: fn = kLdsG8[a.R - 1]; break;
             case TileOrder::kGroup2: fn = kLdsG2[a.R - 1]; break;
             case TileOrder::kSeg8: fn = kLdsQ8[a.R - 1]; break;
             case TileOrder::kSeg16: fn = kLdsQ16[a.R - 1]; break;
+            case TileOrder::kXcd8: fn = kLdsX8[a.R - 1]; break;
+            case TileOrder::kXcd32: fn = kLdsX32[a.R - 1]; break;
             case TileOrder::kConsecutive: break;
           }
           const uint32_t rows = (1u << a.R) - 1;
           const int oi = static_cast<int>(ord);
-          if (a.R <= 4 && (a.verify_mask & rows) && oi >= 0 && oi < 5) fn = kLdsVerify[oi][a.R - 1];
+          if (a.R <= 4 && (a.verify_mask & rows) && oi >= 0 && oi < kTileOrders)
+            fn = kLdsVerify[oi][a.R - 1];
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }
@@ -364,16 +422,24 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         static_assert(LdsPolicy::BS == LdsWidePolicy::BS && LdsPolicy::U == LdsWidePolicy::U &&
                           LdsG8Policy::BS == LdsPolicy::BS && LdsG2Policy::BS == LdsPolicy::BS &&
                           LdsQ8Policy::BS == LdsPolicy::BS && LdsQ16Policy::BS == LdsPolicy::BS &&
+                          LdsX8Policy::BS == LdsPolicy::BS && LdsX32Policy::BS == LdsPolicy::BS &&
                           LdsWideQ8Policy::BS == LdsPolicy::BS &&
                           LdsVerifyPolicy<0>::TILE_VECS == LdsPolicy::TILE_VECS &&
-                          LdsRealignOutPolicy::BS == LdsPolicy::BS &&
-                          LdsRealignOut8Policy::TILE_VECS == LdsRealignOutPolicy::TILE_VECS,
+                          LdsRealignOutPolicy<0>::BS == LdsPolicy::BS &&
+                          LdsRealignOut8Policy<0>::TILE_VECS == LdsRealignOutPolicy<0>::TILE_VECS &&
+                          LdsRealignOutPolicy<10>::TILE_VECS == LdsRealignOutPolicy<0>::TILE_VECS,
                       "one grid shape for every LDS policy");
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         // misaligned shards: the realigning form, unless a tuned order names a plain kernel
-        if (can_realign(a) && (order == kOrderRealign || (order < 0 && takes_realign(a)))) {
-          fn = kLdsRealignOut[a.R - 1];
-          gx = dev::vec_grid<LdsRealignOutPolicy>(a.nvec, a.batch);
+        if (can_realign(a) && (order >= kOrderRealign || (order < 0 && takes_realign(a)))) {
+          if (order >= kOrderStage && can_stage(a)) {
+            fn = kLdsStage[realign_order_index(order)][a.R - 1];
+            gx = dev::vec_grid<LdsStagePolicyFor<8, 0>>(a.nvec, a.batch);
+            lds += dev::lds_stage_bytes(LdsPolicy::BS);
+          } else {
+            fn = kLdsRealignOut[realign_order_index(order)][a.R - 1];
+            gx = dev::vec_grid<LdsRealignOutPolicy<0>>(a.nvec, a.batch);
+          }
           a.tail_in_vec = 1;  // its first tile writes every edge byte, the tail included
           tail0 = a.S;
         }
@@ -430,27 +496,34 @@ constexpr auto nomath_wide_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 9, NomathPolicy<ORD, Rs + 9>>...};
 }
 // [TileOrder][R - 1] for R <= 8; wide groups: consecutive and Q8 (the orders they run)
-const std::array<std::array<VecFn, 8>, 5> kNomath = {
+const std::array<std::array<VecFn, 8>, kTileOrders> kNomath = {
     nomath_table<0>(std::make_integer_sequence<int, 8>{}), nomath_table<2>(std::make_integer_sequence<int, 8>{}),
     nomath_table<5>(std::make_integer_sequence<int, 8>{}), nomath_table<6>(std::make_integer_sequence<int, 8>{}),
-    nomath_table<8>(std::make_integer_sequence<int, 8>{})};
+    nomath_table<8>(std::make_integer_sequence<int, 8>{}), nomath_table<10>(std::make_integer_sequence<int, 8>{}),
+    nomath_table<11>(std::make_integer_sequence<int, 8>{})};
 const auto kNomathWide = nomath_wide_table<0>(std::make_integer_sequence<int, 8>{});
 const auto kNomathWideQ8 = nomath_wide_table<6>(std::make_integer_sequence<int, 8>{});
 static_assert(NomathPolicy<0, 4>::TILE_VECS == LdsPolicy::TILE_VECS &&
                   NomathPolicy<0, 16>::TILE_VECS == LdsPolicy::TILE_VECS && LdsPolicy::BS == 512,
               "the ceilings run the production grid");
 
-const std::array<VecFn, 5> kStreamRead = {&dev::rs_stream_read<0>, &dev::rs_stream_read<2>,
-                                           &dev::rs_stream_read<5>, &dev::rs_stream_read<6>,
-                                           &dev::rs_stream_read<8>};
-const std::array<VecFn, 5> kStreamWrite = {&dev::rs_stream_write<0>, &dev::rs_stream_write<2>,
-                                            &dev::rs_stream_write<5>, &dev::rs_stream_write<6>,
-                                            &dev::rs_stream_write<8>};
+const std::array<VecFn, kTileOrders> kStreamRead = {
+    &dev::rs_stream_read<0>, &dev::rs_stream_read<2>, &dev::rs_stream_read<5>, &dev::rs_stream_read<6>,
+    &dev::rs_stream_read<8>, &dev::rs_stream_read<10>, &dev::rs_stream_read<11>};
+const std::array<VecFn, kTileOrders> kStreamWrite = {
+    &dev::rs_stream_write<0>, &dev::rs_stream_write<2>, &dev::rs_stream_write<5>,
+    &dev::rs_stream_write<6>, &dev::rs_stream_write<8>, &dev::rs_stream_write<10>,
+    &dev::rs_stream_write<11>};
+
+// modes 3..5 (probe): the write streams alone from each row's first 64 / 128 / 256-B
+// boundary, consecutive tiles
+const std::array<VecFn, 3> kStreamWriteAligned = {
+    &dev::rs_stream_write<0, 64>, &dev::rs_stream_write<0, 128>, &dev::rs_stream_write<0, 256>};
 }  // namespace
 
 hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1 || !a.ltabs ||
-      mode < 0 || mode > 2)
+      mode < 0 || mode > 5)
     return hipErrorInvalidValue;
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
@@ -458,11 +531,14 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode) 
   // the order the production launch would take (a tuned order, else the rule; the
   // realigning and v_perm launches are bounded by the plain kernel's traffic)
   const TileOrder ord =
-      a.R <= 8 ? (order >= 0 && order != kOrderRealign ? static_cast<TileOrder>(order) : lds_rule(a))
+      a.R <= 8 ? (order >= kOrderStage ? static_cast<TileOrder>(order - kOrderStage)
+                  : order >= kOrderRealign ? static_cast<TileOrder>(order - kOrderRealign)
+                  : order >= 0 ? static_cast<TileOrder>(order) : lds_rule(a))
                : (order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a));
   const unsigned grid = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
   if (mode > 0) {  // the read streams alone / the write streams alone
-    const VecFn fn = (mode == 1 ? kStreamRead : kStreamWrite)[static_cast<int>(ord)];
+    const VecFn fn = mode >= 3 ? kStreamWriteAligned[mode - 3]
+                               : (mode == 1 ? kStreamRead : kStreamWrite)[static_cast<int>(ord)];
     a.tail_in_vec = 0;
     launch_sliced(grid, a.K + a.R, a, [&](uint32_t blocks) {
       hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), 0, stream, a);

@@ -104,6 +104,9 @@ inline int shard_addr_tz(const void* const* p, int count) {
 // (tile orders are TileOrder values 0..4, which on a misaligned launch select the plain
 // kernel with unaligned accesses)
 constexpr int kOrderRealign = 32;
+// ... and for its form that stages the parity stores through LDS and writes them from
+// 128-B boundaries (rs_apply.hpp REALIGN 4): kOrderStage + the TileOrder it runs in
+constexpr int kOrderStage = 48;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the

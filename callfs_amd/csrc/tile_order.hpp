@@ -21,7 +21,7 @@ namespace callfs {
 template <int ORD>
 CALLFS_HD inline void map_tile(uint32_t t, uint32_t tps, uint32_t batch, uint32_t& stripe,
                                uint32_t& tile) {
-  if constexpr (ORD == 0) {
+  if constexpr (ORD == 0 || ORD >= 10) {  // 10, 11: consecutive after block_tile (below)
     stripe = t / tps;
     tile = t - stripe * tps;
   } else if constexpr (ORD >= 6) {
@@ -44,8 +44,32 @@ CALLFS_HD inline void map_tile(uint32_t t, uint32_t tps, uint32_t batch, uint32_
   }
 }
 
-// Launch-time choice; Policy::ORD of each: consecutive 0, G8 2, G2 5, Q8 6, Q16 8.
-enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16 };
+// XCD-grouped consecutive orders (ORD 10: X8, 11: X32). A dispatch deals its blocks to the
+// 8 XCDs round-robin (block b of the launch runs on XCD b % 8), so in consecutive order
+// the two tiles on either side of every tile boundary of a row run on different XCDs,
+// each with its own L2. Where a row's tile boundaries fall inside a 64-B line (rows at a
+// 16-B-granular pitch, the Split layout), each L2 then writes its part of that line back
+// as a partial write. X8 / X32 give the blocks b, b+8, b+16, ... of every group of 8*J
+// blocks J consecutive tiles (J = 8 / 32), so the tiles in flight are those of
+// consecutive order, permuted within the group, and only one boundary in J crosses XCDs.
+// Blocks past the last full group keep their place. Host-side as well: host_test checks
+// that the map is a bijection.
+template <int ORD>
+CALLFS_HD inline uint32_t block_tile(uint32_t b, uint32_t nblocks) {
+  if constexpr (ORD >= 10) {
+    constexpr uint32_t J = ORD == 10 ? 8 : 32, G = 8 * J;
+    if (b >= nblocks / G * G) return b;
+    const uint32_t g = b / G, r = b - g * G;
+    return g * G + (r & 7u) * J + (r >> 3);
+  } else {
+    return b;
+  }
+}
+
+// Launch-time choice; Policy::ORD of each: consecutive 0, G8 2, G2 5, Q8 6, Q16 8, X8 10,
+// X32 11.
+enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16, kXcd8, kXcd32 };
+constexpr int kTileOrders = 7;
 
 // Tile order for R <= 8 (Policy::ORD; tools/kbench.hip KB_ORD, tools/order_sweep.sh,
 // 5-15 rounds, % of 8 TB/s, DESIGN.md "Tile order"). Neighbouring blocks normally take

@@ -104,7 +104,8 @@ class Plan:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         N.check(N.lib.rs_plan_launch(self.handle, ctypes.c_void_p(s.cuda_stream)), "rs_plan_launch")
 
-    CEILINGS = {"nolookup": 0, "read": 1, "write": 2}
+    CEILINGS = {"nolookup": 0, "read": 1, "write": 2, "write64": 3, "write128": 4,
+                "write256": 5}
 
     def launch_ceiling(self, mode: str = "nolookup",
                        stream: Optional[torch.cuda.Stream] = None) -> None:
@@ -115,9 +116,11 @@ class Plan:
         N.check(N.lib.rs_plan_launch_ceiling(self.handle, ctypes.c_void_p(s.cuda_stream),
                                              self.CEILINGS[mode]), "rs_plan_launch_ceiling")
 
-    # tile orders (RS_ORDER_*); on misaligned shards 0..4 name the plain kernel with
-    # unaligned accesses and "realign" the kernel that aligns loads and stores
-    ORDER_NAMES = {-1: "none", 0: "consecutive", 1: "g8", 2: "g2", 3: "q8", 4: "q16", 32: "realign"}
+    # tile orders (RS_ORDER_*); on misaligned shards 0..6 name the plain kernel with
+    # unaligned accesses and "realign*" the kernel that aligns loads and stores
+    ORDER_NAMES = {-1: "none", 0: "consecutive", 1: "g8", 2: "g2", 3: "q8", 4: "q16", 5: "x8",
+                   6: "x32", 32: "realign", 37: "realign-x8", 38: "realign-x32", 48: "stage",
+                   53: "stage-x8", 54: "stage-x32"}
 
     def tune(self, reps: int = 5, stream: Optional[torch.cuda.Stream] = None) -> list:
         """rs_plan_tune: time each launch group in every tile order its kernel offers
@@ -129,6 +132,14 @@ class Plan:
         N.check(N.lib.rs_plan_tune(self.handle, ctypes.c_void_p(s.cuda_stream), reps, orders, n),
                 "rs_plan_tune")
         return [self.ORDER_NAMES.get(orders[i], str(orders[i])) for i in range(n)]
+
+    def set_orders(self, names: Sequence[str]) -> None:
+        """rs_plan_set_orders: pin launch group i to tile order names[i] ("none" = the
+        rule). An order the group's kernel does not offer raises NativeError (RS_E_ARG)
+        and leaves the plan unchanged."""
+        codes = {v: k for k, v in self.ORDER_NAMES.items()}
+        arr = (ctypes.c_int * len(names))(*[codes[nm] for nm in names])
+        N.check(N.lib.rs_plan_set_orders(self.handle, arr, len(names)), "rs_plan_set_orders")
 
     def corrupt(self, stream: Optional[torch.cuda.Stream] = None) -> bool:
         """Synchronises the stream; True when a Verify row mismatched (then clears)."""

@@ -177,11 +177,23 @@ void rs_plan_destroy(rs_plan* plan);
 #define RS_ORDER_GROUP2 2
 #define RS_ORDER_SEG8 3
 #define RS_ORDER_SEG16 4
+/* consecutive tiles, J = 8 / 32 of them per XCD in turn (DESIGN.md §5 "XCD-grouped") */
+#define RS_ORDER_XCD8 5
+#define RS_ORDER_XCD32 6
 /* misaligned shards (upstream Split layout at odd S): the kernel that realigns loads and
- * parity stores in registers; on such launches RS_ORDER_0..4 name the plain kernel with
- * unaligned 16-B accesses in that tile order */
+ * parity stores in registers, RS_ORDER_REALIGN + the tile order it runs in (consecutive,
+ * XCD8 or XCD32); on such launches RS_ORDER_0..6 name the plain kernel with unaligned
+ * 16-B accesses in that tile order */
 #define RS_ORDER_REALIGN 32
+/* the same loads with the parity stores staged through LDS and written from each row's
+ * first 128-B boundary on, RS_ORDER_STAGE + the tile order it runs in */
+#define RS_ORDER_STAGE 48
 int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups);
+/* Sets the tile order of launch groups 0..n-1 (the others: the rule) to orders[i], as
+ * rs_plan_tune would: RS_ORDER_* that the group's kernel offers (the candidates
+ * rs_plan_tune times), or -1 for the rule. RS_E_ARG if any entry is not offered or n
+ * exceeds rs_plan_groups; the plan is then unchanged. For orders tuned once and kept. */
+int  rs_plan_set_orders(rs_plan* plan, const int* orders, int n);
 /* Measurement only (no upstream counterpart): enqueues the plan's launch groups as a
  * traffic ceiling of the same shape, on the production grid, tile order and slicing, for
  * a roofline denominator measured in the same process (bench.py):
@@ -194,6 +206,11 @@ int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_gr
 #define RS_CEIL_NOLOOKUP 0
 #define RS_CEIL_READ 1
 #define RS_CEIL_WRITE 2
+/* probes: the write streams alone from each row's first 64 / 128 / 256-B boundary on
+ * (every wave's 1 KiB store aligned to that; consecutive tiles) */
+#define RS_CEIL_WRITE_AL64 3
+#define RS_CEIL_WRITE_AL128 4
+#define RS_CEIL_WRITE_AL256 5
 int  rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode);
 /* Launch groups of a plan (the `orders` entries rs_plan_tune can fill): one per up to 16
  * written or compared rows; 0 for a NULL plan. */

@@ -237,6 +237,23 @@ int main() {
         CHECK(bijective(map_tile<8>, tps, b));
         CHECK(bijective(map_tile<9>, tps, b));
       }
+    // XCD-grouped orders: block -> tile index is a bijection on every launch (slice) size,
+    // and blocks b, b + 8 of a full group take neighbouring tiles
+    auto block_bijective = [](auto fn, uint32_t nb) {
+      std::vector<uint8_t> seen(nb, 0);
+      for (uint32_t b = 0; b < nb; ++b) {
+        const uint32_t t = fn(b, nb);
+        if (t >= nb || seen[t]++) return false;
+      }
+      return true;
+    };
+    for (uint32_t nb : {1u, 7u, 8u, 63u, 64u, 65u, 255u, 256u, 257u, 1000u, 4096u, 65536u, 70001u}) {
+      CHECK(block_bijective(block_tile<10>, nb));
+      CHECK(block_bijective(block_tile<11>, nb));
+      CHECK(block_bijective(block_tile<0>, nb));
+    }
+    CHECK(block_tile<10>(3, 64) == 24 && block_tile<10>(11, 64) == 25 && block_tile<10>(64, 128) == 64);
+    CHECK(block_tile<11>(1, 256) == 32 && block_tile<11>(9, 256) == 33 && block_tile<11>(5, 255) == 5);
     // rules, on layouts measured in DESIGN.md §5 (tps = S / 8 KiB)
     auto tps_of = [](uint64_t S) { return (S / 16 + 511) / 512; };
     const uint64_t MiB = 1ull << 20;

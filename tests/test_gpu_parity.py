@@ -1179,7 +1179,7 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
     enc = Plan.for_batch(sb)
     names = enc.tune(reps=1)
     assert len(names) == max(1, -(-m // 16))
-    assert all(n in {"consecutive", "g8", "g2", "q8", "q16"} for n in names), names
+    assert all(n in {"consecutive", "g8", "g2", "q8", "q16", "x8", "x32"} for n in names), names
     sb.fill_random(S + k + 1)  # fresh data: the tuned plan must compute it, not reuse
     enc.launch()
     torch.cuda.synchronize()
@@ -1207,6 +1207,74 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
     assert dec.corrupt_stripes() == [1]
 
 
+ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign",
+                   "realign-x8", "realign-x32", "stage", "stage-x8", "stage-x32"]
+
+
+@pytest.mark.parametrize("k,m,S,batch,off,erase", [
+    (10, 4, (1 << 20) + 16, 3, 0, None),   # aligned: 129 tiles per stripe, X8/X32 groups + tail
+    (10, 4, (1 << 20) + 1, 3, 1, None),    # Split layout (odd S): realigning kernel per order
+    (10, 4, (1 << 20) + 1, 3, 1, (5,)),    # one erasure: 1 written + 3 Verify rows
+    (10, 8, 300_001, 5, 3, None),          # R = 8, realigning kernel
+    (4, 2, 8 * 512 * 16 * 9 + 7, 2, 0, (0, 1)),  # k = 4, R = 2 decode, ragged tail
+])
+def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, erase):
+    """rs_plan_set_orders pins each tile order the launch group's kernel offers (the
+    rs_plan_tune candidates, X8 / X32 and the realigning kernel's orders included); every
+    instance recomputes every byte of every stripe as the oracle does, Verify rows pass on
+    clean stripes and flag a flipped byte. An order the kernel does not offer is refused
+    (RS_E_ARG) and leaves the plan as it was."""
+    import torch
+    from callfs_amd import _native as N
+    from callfs_amd.device import Plan
+    n = k + m
+    total = batch * n * S
+    buf = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device="cuda:0")
+    base = buf.data_ptr() + off
+    ptrs = [base + (b * n + i) * S for b in range(batch) for i in range(n)]
+    host = buf.cpu().numpy()[off:off + total].copy()
+    for b in range(batch):  # consistent stripes: oracle parity in place
+        st = host[b * n * S:(b + 1) * n * S]
+        want = cref.encode([st[i * S:(i + 1) * S] for i in range(k)], k, m)
+        for j in range(m):
+            st[(k + j) * S:(k + j + 1) * S] = want[j]
+    good = torch.from_numpy(host).to("cuda:0")
+    present = None if erase is None else [i not in erase for i in range(n)]
+    plan = Plan(k, m, S, batch, ptrs, present=present)
+    taken = []
+    for name in ALL_ORDER_NAMES:
+        try:
+            plan.set_orders([name])
+        except N.NativeError as e:
+            assert e.code == N.RS_E_ARG
+            continue
+        taken.append(name)
+        buf[off:off + total].copy_(good)
+        for i in (range(k, n) if erase is None else erase):
+            for b in range(batch):
+                s0 = off + (b * n + i) * S
+                buf[s0:s0 + S].zero_()
+        plan.launch()
+        assert not plan.corrupt(), name
+        assert torch.equal(buf[off:off + total], good), name
+        if erase is not None and (n - len(erase)) > k:  # a Verify row exists: flip in it
+            vrow = max(i for i in range(n) if i not in erase)
+            buf[off + (1 * n + vrow) * S + S // 2] ^= 0x40
+            plan.launch()
+            assert plan.corrupt_stripes() == [1], name
+    assert "consecutive" in taken or "realign" in taken, taken
+    if (off | S) % 2:  # shards at odd offsets
+        assert {"realign", "realign-x8", "realign-x32", "stage", "stage-x8",
+                "stage-x32"} <= set(taken), taken
+    else:
+        assert {"x8", "x32"} <= set(taken), taken
+        with pytest.raises(N.NativeError):
+            plan.set_orders(["realign"])  # aligned shards: no realigning kernel
+    with pytest.raises(N.NativeError):
+        plan.set_orders(["none"] * (plan_groups := int(N.lib.rs_plan_groups(plan.handle))) + ["none"])
+    plan.set_orders(["none"] * plan_groups)
+
+
 def test_plan_tune_argument_errors(native_lib):
     import ctypes
     from callfs_amd import _native as N
@@ -1218,7 +1286,7 @@ def test_plan_tune_argument_errors(native_lib):
     assert N.lib.rs_plan_tune(None, None, 1, None, 0) == N.RS_E_ARG
     out = (ctypes.c_int * 3)(-7, -7, -7)
     assert N.lib.rs_plan_tune(p.handle, None, 1, out, 3) == 0
-    assert out[0] in range(5) and out[1] == -1 and out[2] == -1
+    assert out[0] in range(7) and out[1] == -1 and out[2] == -1
 
 
 @pytest.mark.parametrize("k,m,S,batch,off", [(10, 4, 100_003, 3, 3), (4, 2, 65_537, 5, 1),
@@ -1236,7 +1304,7 @@ def test_plan_tune_misaligned_split_layout(native_lib, k, m, S, batch, off):
     ptrs = [base + (b * n + i) * S for b in range(batch) for i in range(n)]
     enc = Plan(k, m, S, batch, ptrs)
     names = enc.tune(reps=1)
-    assert all(x in {"realign", "consecutive", "g8", "g2", "q8", "q16"} for x in names), names
+    assert all(x in set(ALL_ORDER_NAMES) for x in names), names
     buf[off:off + total].copy_(torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda:0"))
     enc.launch()
     torch.cuda.synchronize()
