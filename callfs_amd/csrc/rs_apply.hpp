@@ -117,17 +117,11 @@ struct Policy {
   // LDS table addresses by v_or_b32_sdwa (byte select + OR) instead of v_perm_b32
   static constexpr bool SDWA = SDWA_;
   // 0: plain; 1: aligned loads realigned in registers (63 vectors per wave); 2: loads and
-  // parity stores both aligned (62 vectors per wave, edge bytes in the first tile);
-  // 4: REALIGN 1's loads, parity stores staged through LDS and written from each row's
-  // first 128-B boundary on (every wave's 1 KiB store 128-B aligned; lds_stage_store)
+  // parity stores both aligned (62 vectors per wave, edge bytes in the first tile)
   static constexpr int REALIGN = REALIGN_;
-  // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads;
-  // REALIGN 4 tiles are 8 vectors shorter than their waves' 8 x 63 results, so that a
-  // row's 128-B-aligned store window, up to 127 bytes past the tile, has its results
+  // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads
   static constexpr int WAVE_VECS = REALIGN_ == 2 ? 62 : (REALIGN_ || PROBE_ == 1) ? 63 : 64;
-  static constexpr int TILE_VECS = REALIGN_ == 4      ? BS_ / 64 * 63 - 8
-                                   : WAVE_VECS < 64 ? BS_ / 64 * WAVE_VECS
-                                                    : BS_ * U_;
+  static constexpr int TILE_VECS = WAVE_VECS < 64 ? BS_ / 64 * WAVE_VECS : BS_ * U_;
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
   static constexpr bool NT_LOAD = NT_LOAD_;
@@ -435,13 +429,8 @@ struct LdsAcc {
 template <class T>
 using lds_ptr = const __attribute__((address_space(3))) T*;
 
-// Dynamic LDS bytes of rs_apply_lds's tables for K input shards and RT rows (REALIGN 4
-// adds its staging slots after them: lds_stage_bytes).
-__host__ __device__ inline size_t lds_bytes(int K, int RT) {
-  return static_cast<size_t>(K) * 32 * (RT > 8 ? 16 : 8);
-}
-constexpr int kStageRows = 4;  // REALIGN 4: rows staged per block barrier
-inline size_t lds_stage_bytes(int BS) { return static_cast<size_t>(kStageRows) * (BS / 64 * 63) * 16; }
+// Dynamic LDS bytes of rs_apply_lds for K input shards and RT rows.
+inline size_t lds_bytes(int K, int RT) { return static_cast<size_t>(K) * 32 * (RT > 8 ? 16 : 8); }
 
 // One table entry at an absolute 32-bit LDS address (no base add per lookup).
 template <int RT>
@@ -653,73 +642,6 @@ __device__ __forceinline__ void lds_edges(const ApplyArgs& a, cptr<const uint8_t
   if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
 }
 
-// ---- parity stores from 128-B boundaries (Policy::REALIGN == 4) ------------------------
-// A wave-instruction's 1 KiB store that starts off a 128-B boundary writes at 60-64 % of
-// spec alone, from a 128-B boundary at 74-75 % (tools/write_align_probe.py, Split layout
-// and 16-B pitches). The rows of a stripe sit at different offsets mod 128, so no tiling
-// of the vectors aligns them all: each written row r is staged through LDS and stored
-// from h_r = (-q_r) & 127 on (q_r = the row's address). A tile of TV = 496 vectors at T0
-// (TV a multiple of 8: the same h_r in every tile) stores the 496 16-B blocks at shard
-// bytes 16 T0 + h_r + 16 j, j < 496, and block j needs results T0 + (h_r >> 4) + j and the
-// next: up to T0 + 503, which its 8 waves x 63 results cover. Thread j reads the two
-// 16-B slots from LDS and funnel-shifts them by h_r & 15. Blocks past the row's last
-// full vector are not stored; lds_edges128 writes the head [0, h_r) and that tail.
-template <int BS>
-constexpr int stage_slots() { return BS / 64 * 63; }
-// bytes [sh, sh + 16) of A:B (sh in 0..15)
-__device__ __forceinline__ uint4 funnel_bytes(const uint4& A, const uint4& B, uint32_t sh) {
-  const uint32_t r = sh & 3u;
-  switch (sh >> 2) {
-    case 0: return funnel16<0>(A, B, r);
-    case 1: return funnel16<1>(A, B, r);
-    case 2: return funnel16<2>(A, B, r);
-    default: return funnel16<3>(A, B, r);
-  }
-}
-
-// Edge bytes of a REALIGN == 4 launch, one byte position per thread: threads 0..127 take
-// bytes 0..127, threads 128..159 the bytes from max(128, 16 nvec - 16) on (< 32 of them:
-// S < 16 nvec + 16). Written row r owns [0, h_r) and [E_r, S), E_r = the end of its last
-// stored block; Verify rows own [16 nvec, S) (their vectors are compared in place).
-template <int RT>
-__device__ __forceinline__ void lds_edges128(const ApplyArgs& a, cptr<const uint8_t*> in,
-                                             cptr<uint8_t*> out, uint32_t stripe, uint32_t lds0) {
-  constexpr int W = LdsAcc<RT>::W;
-  const uint32_t j = threadIdx.x;
-  if (j >= 160u) return;
-  const uint64_t full = a.nvec * 16;  // nvec >= 1 on this path
-  const uint64_t tb = full - 16 > 128 ? full - 16 : 128;
-  const uint64_t b = j < 128u ? j : tb + (j - 128u);
-  if (b >= a.S) return;
-  typename LdsAcc<RT>::T t = lds_zero<RT>();
-  for (int i0 = 0; i0 < a.K; i0 += tail_loads<RT>()) {
-    uint32_t x[tail_loads<RT>()];
-    tail_bytes<RT>(in, b, i0, a.K, x);
-    for (int jj = 0; jj < tail_loads<RT>() && i0 + jj < a.K; ++jj) {
-      const uint32_t base = lds0 + static_cast<uint32_t>(i0 + jj) * 32u * W;
-      t = t ^ lds_lookup<RT>(base + (x[jj] & 15u) * W) ^
-          lds_lookup<RT>(base + 16u * W + (x[jj] >> 4) * W);
-    }
-  }
-  bool bad = false;
-  for (int r = 0; r < a.R && r < RT; ++r) {
-    const uint8_t v = static_cast<uint8_t>(lds_byte<RT>(t, r));
-    const bool verify = (a.verify_mask >> r) & 1u;
-    bool mine;
-    if (verify) {
-      mine = b >= full;
-    } else {
-      const uint64_t h = (0u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r]))) & 127u;
-      const uint64_t e = full >= h ? h + ((full - h) & ~uint64_t(15)) : h;
-      mine = b < h || b >= e;
-    }
-    if (!mine) continue;
-    if (verify) bad |= out[r][b] != v;
-    else out[r][b] = v;
-  }
-  if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
-}
-
 // Waves per SIMD the LDS kernel may be limited to: 16-byte entries keep 8 b128 reads
 // (32 VGPRs) in flight, which the register allocator only grants below 5 waves.
 template <int RT>
@@ -762,9 +684,7 @@ void rs_apply_lds(ApplyArgs a) {
                                 : static_cast<uint64_t>(tile) * BS + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * R;
-    if constexpr (P::REALIGN == 4) {
-      if (tile == 0) lds_edges128<RT>(a, in, out, stripe, lds0);
-    } else if constexpr (P::REALIGN == 2) {
+    if constexpr (P::REALIGN == 2) {
       if (tile == 0) lds_edges<RT>(a, in, out, stripe, lds0);
     } else {
       if (tile == 0 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
@@ -772,9 +692,7 @@ void rs_apply_lds(ApplyArgs a) {
     // lanes that store (REALIGN: lane 63 -- REALIGN 2: lanes 62, 63 -- and lanes past the
     // shard only load)
     const bool active = v0 < a.nvec && lane < WV && !(P::PROBE == 2 && lane == 63u);
-    // REALIGN: whole wave idle (REALIGN 4 never leaves: its waves meet at block barriers;
-    // an idle wave's loads are clamped into the shard and its results never stored)
-    if (P::REALIGN != 4 && (P::REALIGN ? (v0 - lane >= a.nvec) : !active)) continue;
+    if (P::REALIGN ? (v0 - lane >= a.nvec) : !active) continue;  // REALIGN: whole wave idle
     auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
     AccT acc[4][4];
 #pragma unroll
@@ -856,9 +774,6 @@ void rs_apply_lds(ApplyArgs a) {
       const uint4 o = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
                                  lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
       uint4* dst = reinterpret_cast<uint4*>(out[r]) + v0;
-      if constexpr (P::REALIGN == 4) {
-        if (!((a.verify_mask >> r) & 1u)) continue;  // written rows: staged below
-      }
       if constexpr (P::REALIGN == 2) {
         if (!((a.verify_mask >> r) & 1u)) {
           const uint32_t mo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r])) & 15u;
@@ -887,49 +802,6 @@ void rs_apply_lds(ApplyArgs a) {
       }
     }
     if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
-    if constexpr (P::REALIGN == 4) {
-      // written rows through LDS, kStageRows per barrier (block-uniform branches: R and
-      // verify_mask are kernel arguments)
-      constexpr int NS = stage_slots<BS>();
-      static_assert(TV % 8 == 0 && TV + 8 <= NS, "128-B windows need 8 spare results");
-      const uint32_t st0 = lds0 + static_cast<uint32_t>(lds_bytes(K, RT));
-      const uint32_t wave = threadIdx.x >> 6;
-#pragma unroll
-      for (int r0 = 0; r0 < RT; r0 += kStageRows) {
-        if (r0 >= R) break;
-        if (r0 > 0) __syncthreads();  // the previous rows' slots have been read
-#pragma unroll
-        for (int c = 0; c < kStageRows; ++c) {
-          const int r = r0 + c;
-          if (r >= RT || r >= R || ((a.verify_mask >> r) & 1u)) continue;
-          const uint4 o = make_uint4(lds_row<RT>(acc[0], r), lds_row<RT>(acc[1], r),
-                                     lds_row<RT>(acc[2], r), lds_row<RT>(acc[3], r));
-          if (lane < 63u) {
-            const uint32_t ad = st0 + (static_cast<uint32_t>(c) * NS + wave * 63u + lane) * 16u;
-            *(__attribute__((address_space(3))) u32x4*)(static_cast<uintptr_t>(ad)) =
-                u32x4{o.x, o.y, o.z, o.w};
-          }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int c = 0; c < kStageRows; ++c) {
-          const int r = r0 + c;
-          if (r >= RT || r >= R || ((a.verify_mask >> r) & 1u)) continue;
-          const uint32_t h = (0u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out[r]))) & 127u;
-          const uint32_t j = threadIdx.x;
-          const uint64_t p = (static_cast<uint64_t>(tile) * TV + j) * 16u + h;  // shard byte
-          if (j >= static_cast<uint32_t>(TV) || p + 16 > a.nvec * 16) continue;
-          const uint32_t ad = st0 + (static_cast<uint32_t>(c) * NS + (h >> 4) + j) * 16u;
-          const u32x4 A = *(lds_ptr<u32x4>)(static_cast<uintptr_t>(ad));
-          uint4 X = make_uint4(A.x, A.y, A.z, A.w);
-          if (h & 15u) {
-            const u32x4 B = *(lds_ptr<u32x4>)(static_cast<uintptr_t>(ad + 16u));
-            X = funnel_bytes(X, make_uint4(B.x, B.y, B.z, B.w), h & 15u);
-          }
-          store16<P>(reinterpret_cast<uint4*>(out[r] + p), X);  // 16-B (128-B per wave) aligned
-        }
-      }
-    }
   }
 }
 
@@ -949,14 +821,22 @@ __device__ __forceinline__ const uint4* align16(const uint8_t* p) {
   return reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
 }
 
-template <int ORD>
+// AL > 16 (measurement probe): each shard is read from its first AL-byte boundary on, so
+// every wave-instruction's 1 KiB load starts on an AL-byte boundary
+template <int AL>
+__device__ __forceinline__ const uint4* align_read(const uint8_t* p) {
+  if constexpr (AL == 16) return align16(p);
+  else return reinterpret_cast<const uint4*>((reinterpret_cast<uintptr_t>(p) + AL - 1) & ~uintptr_t(AL - 1));
+}
+
+template <int ORD, int AL = 16>
 __global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
   const uint32_t tps = static_cast<uint32_t>((a.nvec + 511) / 512);
   uint32_t stripe, tile;
   map_tile<ORD>(a.t_base + block_tile<ORD>(blockIdx.x, gridDim.x), tps,
                 static_cast<uint32_t>(a.batch), stripe, tile);
   const uint64_t v0 = static_cast<uint64_t>(tile) * 512 + threadIdx.x;
-  if (v0 >= a.nvec) return;
+  if (v0 + (AL > 16 ? AL / 16 : 0) >= a.nvec) return;
   cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * a.K;
   cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * a.R;
   using P = Policy<2, 1, true, true, false, 512>;
@@ -969,7 +849,7 @@ __global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
     uint4 x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (i0 + j < a.K) x[j] = load16<P>(align16(in[i0 + j]) + v0);
+      if (i0 + j < a.K) x[j] = load16<P>(align_read<AL>(in[i0 + j]) + v0);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (i0 + j < a.K) mix(x[j]);
@@ -979,7 +859,7 @@ __global__ __launch_bounds__(512) void rs_stream_read(ApplyArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (r0 + j < a.R && ((a.verify_mask >> (r0 + j)) & 1u))
-        x[j] = load16<P>(align16(out[r0 + j]) + v0);
+        x[j] = load16<P>(align_read<AL>(out[r0 + j]) + v0);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (r0 + j < a.R && ((a.verify_mask >> (r0 + j)) & 1u)) mix(x[j]);

@@ -1604,7 +1604,7 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
 
 int rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode) {
   DeviceGuard dg;
-  if (!plan || mode < 0 || mode > 5) return RS_E_ARG;
+  if (!plan || mode < 0 || mode > 8) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
   std::vector<int> orders;
   {
@@ -1751,7 +1751,7 @@ int rs_plan_set_orders(rs_plan* plan, const int* orders, int n) {
   for (int gi = 0; gi < n; ++gi) {
     if (orders[gi] == -1) continue;
     const ApplyArgs a = group_args(t, plan->layout, gi, plan->batch, d, plan->S, 1, plan->hint);
-    const std::vector<int> cand = order_candidates(a);
+    const std::vector<int> cand = order_candidates(a, /*every_instance=*/true);
     if (std::find(cand.begin(), cand.end(), orders[gi]) == cand.end()) return RS_E_ARG;
     next[gi] = orders[gi];
   }

@@ -88,10 +88,6 @@ using LdsRealignOut8Policy = dev::Policy<8, 1, true, true, false, 512, 2, ORD, 0
 template <int R, int ORD>
 using LdsRealignOutPolicyFor =
     typename std::conditional<(R <= 4), LdsRealignOut8Policy<ORD>, LdsRealignOutPolicy<ORD>>::type;
-// The same loads with the parity stores staged through LDS and written from each row's
-// first 128-B boundary (rs_apply.hpp REALIGN 4).
-template <int R, int ORD>
-using LdsStagePolicyFor = dev::Policy<(R <= 4 ? 8 : 6), 1, true, true, false, 512, 2, ORD, 0, false, 4>;
 // CALLFS_RS_TILE_ORDER=consecutive|g8|g2|q8|q16|x8|x32 overrides the rule for every LDS-kernel
 // launch with R <= 8 (A/B on a deployment's own shard layout; unset = the rule).
 int tile_order_override() {
@@ -210,15 +206,6 @@ template <int ORD, int... Rs>
 constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1, ORD>>...};
 }
-template <int ORD, int... Rs>
-constexpr auto lds_stage_table(std::integer_sequence<int, Rs...>) {
-  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsStagePolicyFor<Rs + 1, ORD>>...};
-}
-// [consecutive, X8, X32][R - 1]
-const std::array<std::array<VecFn, 8>, 3> kLdsStage = {
-    lds_stage_table<0>(std::make_integer_sequence<int, 8>{}),
-    lds_stage_table<10>(std::make_integer_sequence<int, 8>{}),
-    lds_stage_table<11>(std::make_integer_sequence<int, 8>{})};
 // [consecutive, X8, X32][R - 1]
 const std::array<std::array<VecFn, 8>, 3> kLdsRealignOut = {
     lds_realign_out_table<0>(std::make_integer_sequence<int, 8>{}),
@@ -310,25 +297,21 @@ bool takes_realign(const ApplyArgs& a) {
   return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u);
 }
 
-// The staging form needs its tables and 4 rows of staging slots in the default 64 KiB of
-// dynamic LDS (k <= 130 at R <= 8)
-bool can_stage(const ApplyArgs& a) {
-  return can_realign(a) && dev::lds_bytes(a.K, a.R) + dev::lds_stage_bytes(LdsPolicy::BS) <= (64u << 10);
-}
-
-// The realigning kernel's tile order: consecutive, or X8 / X32 when CALLFS_RS_TILE_ORDER
-// names them; a tuned realign code (kOrderRealign + TileOrder) names it directly.
-// Returns the index into kLdsRealignOut.
+// The realigning kernel's tile order (index into kLdsRealignOut): a tuned realign code
+// (kOrderRealign + TileOrder) names it; otherwise CALLFS_RS_TILE_ORDER=consecutive / x8
+// / x32, else X32 (DESIGN.md §5 "XCD-grouped tile orders": tools/order_ab.py, Split
+// layout, % of 8 TB/s, two runs, consecutive -> X32: RS(10,4) 64 MiB objects 68.3 /
+// 68.6 -> 69.5 / 69.9, RS(4,2) 1,048,577 B 67.1 / 66.8 -> 68.6 / 68.3, RS(12,4) S =
+// 5,592,406 65.5 / 65.9 -> 66.9 / 66.9, the other five shapes -0.2 ... +0.9).
 int realign_order_index(int order) {
-  const int o = order >= kOrderStage     ? order - kOrderStage
-                : order >= kOrderRealign ? order - kOrderRealign
-                                         : tile_order_override();
-  return o == static_cast<int>(TileOrder::kXcd8) ? 1 : o == static_cast<int>(TileOrder::kXcd32) ? 2 : 0;
+  const int o = order >= kOrderRealign ? order - kOrderRealign : tile_order_override();
+  if (o == static_cast<int>(TileOrder::kConsecutive)) return 0;
+  return o == static_cast<int>(TileOrder::kXcd8) ? 1 : 2;
 }
 
 }  // namespace
 
-std::vector<int> order_candidates(const ApplyArgs& a0) {
+std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
   ApplyArgs a = a0;
   a.nvec = a.S / 16;
   std::vector<int> c;
@@ -345,17 +328,15 @@ std::vector<int> order_candidates(const ApplyArgs& a0) {
       add(TileOrder::kSeg8);
       return c;
     }
-    if (takes_realign(a)) add(static_cast<TileOrder>(kOrderRealign));
+    const auto realign_in = [](TileOrder o) {
+      return static_cast<TileOrder>(kOrderRealign + static_cast<int>(o));
+    };
+    if (takes_realign(a)) add(realign_in(TileOrder::kXcd32));
     add(lds_rule(a));
     if (can_realign(a)) {
-      add(static_cast<TileOrder>(kOrderRealign));
-      add(static_cast<TileOrder>(kOrderRealign + static_cast<int>(TileOrder::kXcd8)));
-      add(static_cast<TileOrder>(kOrderRealign + static_cast<int>(TileOrder::kXcd32)));
-      if (can_stage(a)) {
-        add(static_cast<TileOrder>(kOrderStage));
-        add(static_cast<TileOrder>(kOrderStage + static_cast<int>(TileOrder::kXcd8)));
-        add(static_cast<TileOrder>(kOrderStage + static_cast<int>(TileOrder::kXcd32)));
-      }
+      add(realign_in(TileOrder::kXcd32));
+      add(realign_in(TileOrder::kConsecutive));
+      if (every_instance) add(realign_in(TileOrder::kXcd8));
     }
     add(TileOrder::kConsecutive);
     add(TileOrder::kGroup2);
@@ -364,8 +345,10 @@ std::vector<int> order_candidates(const ApplyArgs& a0) {
       add(TileOrder::kSeg8);
       add(TileOrder::kSeg16);
     }
-    add(TileOrder::kXcd8);
-    add(TileOrder::kXcd32);
+    if (every_instance) {  // never faster than the rule's order on aligned shards
+      add(TileOrder::kXcd8);
+      add(TileOrder::kXcd32);
+    }
     return c;
   }
   add(vec_rule(a));
@@ -391,7 +374,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         a.tail_in_vec = tail0 < a.S;
         if (a.tail_in_vec) tail0 = a.S;
         if (!a.ltabs) return hipErrorInvalidValue;
-        size_t lds = dev::lds_bytes(a.K, a.R);
+        const size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
           const TileOrder ord =
@@ -432,14 +415,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         // misaligned shards: the realigning form, unless a tuned order names a plain kernel
         if (can_realign(a) && (order >= kOrderRealign || (order < 0 && takes_realign(a)))) {
-          if (order >= kOrderStage && can_stage(a)) {
-            fn = kLdsStage[realign_order_index(order)][a.R - 1];
-            gx = dev::vec_grid<LdsStagePolicyFor<8, 0>>(a.nvec, a.batch);
-            lds += dev::lds_stage_bytes(LdsPolicy::BS);
-          } else {
-            fn = kLdsRealignOut[realign_order_index(order)][a.R - 1];
-            gx = dev::vec_grid<LdsRealignOutPolicy<0>>(a.nvec, a.batch);
-          }
+          fn = kLdsRealignOut[realign_order_index(order)][a.R - 1];
+          gx = dev::vec_grid<LdsRealignOutPolicy<0>>(a.nvec, a.batch);
           a.tail_in_vec = 1;  // its first tile writes every edge byte, the tail included
           tail0 = a.S;
         }
@@ -519,25 +496,32 @@ const std::array<VecFn, kTileOrders> kStreamWrite = {
 // boundary, consecutive tiles
 const std::array<VecFn, 3> kStreamWriteAligned = {
     &dev::rs_stream_write<0, 64>, &dev::rs_stream_write<0, 128>, &dev::rs_stream_write<0, 256>};
+// modes 6..8 (probe): the read streams alone from each shard's first 64 / 128 / 256-B boundary
+const std::array<VecFn, 3> kStreamReadAligned = {
+    &dev::rs_stream_read<0, 64>, &dev::rs_stream_read<0, 128>, &dev::rs_stream_read<0, 256>};
 }  // namespace
 
 hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1 || !a.ltabs ||
-      mode < 0 || mode > 5)
+      mode < 0 || mode > 8)
     return hipErrorInvalidValue;
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
   a.tail_in_vec = a.nvec * 16 < a.S;
   // the order the production launch would take (a tuned order, else the rule; the
   // realigning and v_perm launches are bounded by the plain kernel's traffic)
+  static constexpr TileOrder kRealignOrders[3] = {TileOrder::kConsecutive, TileOrder::kXcd8,
+                                                 TileOrder::kXcd32};
+  const bool realign = a.R <= 8 && can_realign(a) &&
+                       (order >= kOrderRealign || (order < 0 && takes_realign(a)));
   const TileOrder ord =
-      a.R <= 8 ? (order >= kOrderStage ? static_cast<TileOrder>(order - kOrderStage)
-                  : order >= kOrderRealign ? static_cast<TileOrder>(order - kOrderRealign)
-                  : order >= 0 ? static_cast<TileOrder>(order) : lds_rule(a))
-               : (order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a));
+      realign    ? kRealignOrders[realign_order_index(order)]
+      : a.R <= 8 ? (order >= 0 ? static_cast<TileOrder>(order) : lds_rule(a))
+                 : (order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a));
   const unsigned grid = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
   if (mode > 0) {  // the read streams alone / the write streams alone
-    const VecFn fn = mode >= 3 ? kStreamWriteAligned[mode - 3]
+    const VecFn fn = mode >= 6   ? kStreamReadAligned[mode - 6]
+                     : mode >= 3 ? kStreamWriteAligned[mode - 3]
                                : (mode == 1 ? kStreamRead : kStreamWrite)[static_cast<int>(ord)];
     a.tail_in_vec = 0;
     launch_sliced(grid, a.K + a.R, a, [&](uint32_t blocks) {

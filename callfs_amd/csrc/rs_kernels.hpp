@@ -103,10 +103,8 @@ inline int shard_addr_tz(const void* const* p, int count) {
 // order_candidates / launch_apply code for the realigning kernel of misaligned launches
 // (tile orders are TileOrder values 0..4, which on a misaligned launch select the plain
 // kernel with unaligned accesses)
+// (kOrderRealign + the TileOrder it runs in: consecutive, X8 or X32)
 constexpr int kOrderRealign = 32;
-// ... and for its form that stages the parity stores through LDS and writes them from
-// 128-B boundaries (rs_apply.hpp REALIGN 4): kOrderStage + the TileOrder it runs in
-constexpr int kOrderStage = 48;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the
@@ -115,8 +113,9 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false
 
 // Tile orders worth timing for launch `a` (rs_plan_tune): the rule's choice first, then
 // the alternatives that have kernel instances for this path. Empty when the launch has
-// no choice (byte kernel, realigning kernel, S < 16).
-std::vector<int> order_candidates(const ApplyArgs& a);
+// no choice (byte kernel, realigning kernel, S < 16). every_instance: also the orders
+// that have an instance but never measured faster (rs_plan_set_orders accepts them).
+std::vector<int> order_candidates(const ApplyArgs& a, bool every_instance = false);
 
 // Measurement only (rs_plan_launch_ceiling), for launch `a` in the order the production
 // launch takes (`order` as for launch_apply), on the production grid and slicing:

@@ -105,7 +105,7 @@ class Plan:
         N.check(N.lib.rs_plan_launch(self.handle, ctypes.c_void_p(s.cuda_stream)), "rs_plan_launch")
 
     CEILINGS = {"nolookup": 0, "read": 1, "write": 2, "write64": 3, "write128": 4,
-                "write256": 5}
+                "write256": 5, "read64": 6, "read128": 7, "read256": 8}
 
     def launch_ceiling(self, mode: str = "nolookup",
                        stream: Optional[torch.cuda.Stream] = None) -> None:
@@ -119,8 +119,7 @@ class Plan:
     # tile orders (RS_ORDER_*); on misaligned shards 0..6 name the plain kernel with
     # unaligned accesses and "realign*" the kernel that aligns loads and stores
     ORDER_NAMES = {-1: "none", 0: "consecutive", 1: "g8", 2: "g2", 3: "q8", 4: "q16", 5: "x8",
-                   6: "x32", 32: "realign", 37: "realign-x8", 38: "realign-x32", 48: "stage",
-                   53: "stage-x8", 54: "stage-x32"}
+                   6: "x32", 32: "realign", 37: "realign-x8", 38: "realign-x32"}
 
     def tune(self, reps: int = 5, stream: Optional[torch.cuda.Stream] = None) -> list:
         """rs_plan_tune: time each launch group in every tile order its kernel offers

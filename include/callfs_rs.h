@@ -185,13 +185,10 @@ void rs_plan_destroy(rs_plan* plan);
  * XCD8 or XCD32); on such launches RS_ORDER_0..6 name the plain kernel with unaligned
  * 16-B accesses in that tile order */
 #define RS_ORDER_REALIGN 32
-/* the same loads with the parity stores staged through LDS and written from each row's
- * first 128-B boundary on, RS_ORDER_STAGE + the tile order it runs in */
-#define RS_ORDER_STAGE 48
 int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups);
 /* Sets the tile order of launch groups 0..n-1 (the others: the rule) to orders[i], as
- * rs_plan_tune would: RS_ORDER_* that the group's kernel offers (the candidates
- * rs_plan_tune times), or -1 for the rule. RS_E_ARG if any entry is not offered or n
+ * rs_plan_tune would: RS_ORDER_* that the group's kernel has an instance of (what
+ * rs_plan_tune times, and XCD8 / XCD32 on aligned shards), or -1 for the rule. RS_E_ARG if any entry is not offered or n
  * exceeds rs_plan_groups; the plan is then unchanged. For orders tuned once and kept. */
 int  rs_plan_set_orders(rs_plan* plan, const int* orders, int n);
 /* Measurement only (no upstream counterpart): enqueues the plan's launch groups as a
@@ -211,6 +208,10 @@ int  rs_plan_set_orders(rs_plan* plan, const int* orders, int n);
 #define RS_CEIL_WRITE_AL64 3
 #define RS_CEIL_WRITE_AL128 4
 #define RS_CEIL_WRITE_AL256 5
+/* probes: the read streams alone from each shard's first 64 / 128 / 256-B boundary on */
+#define RS_CEIL_READ_AL64 6
+#define RS_CEIL_READ_AL128 7
+#define RS_CEIL_READ_AL256 8
 int  rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode);
 /* Launch groups of a plan (the `orders` entries rs_plan_tune can fill): one per up to 16
  * written or compared rows; 0 for a NULL plan. */

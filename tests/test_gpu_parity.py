@@ -1208,7 +1208,7 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
 
 
 ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign",
-                   "realign-x8", "realign-x32", "stage", "stage-x8", "stage-x32"]
+                   "realign-x8", "realign-x32"]
 
 
 @pytest.mark.parametrize("k,m,S,batch,off,erase", [
@@ -1264,8 +1264,7 @@ def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, era
             assert plan.corrupt_stripes() == [1], name
     assert "consecutive" in taken or "realign" in taken, taken
     if (off | S) % 2:  # shards at odd offsets
-        assert {"realign", "realign-x8", "realign-x32", "stage", "stage-x8",
-                "stage-x32"} <= set(taken), taken
+        assert {"realign", "realign-x8", "realign-x32"} <= set(taken), taken
     else:
         assert {"x8", "x32"} <= set(taken), taken
         with pytest.raises(N.NativeError):
@@ -1351,7 +1350,11 @@ def test_plan_ceiling_modes_then_relaunch(native_lib, k, m, S, batch, erase):
     plan.launch_ceiling("read")
     torch.cuda.synchronize()
     assert torch.equal(sb.buf, before)
-    for mode in ("write", "nolookup"):
+    for mode in ("read64", "read128", "read256"):  # alignment probes: read only
+        plan.launch_ceiling(mode)
+        torch.cuda.synchronize()
+        assert torch.equal(sb.buf, before), mode
+    for mode in ("write", "nolookup", "write64", "write128", "write256"):
         plan.launch_ceiling(mode)
         plan.corrupt()  # the no-lookup form compares junk: clear
         plan.launch()
@@ -1362,7 +1365,8 @@ def test_plan_ceiling_modes_then_relaunch(native_lib, k, m, S, batch, erase):
     want = cref.encode([host[0, i] for i in range(k)], k, m)
     for j in range(m):
         assert np.array_equal(host[0, k + j], want[j]), j
-    assert N.lib.rs_plan_launch_ceiling(plan.handle, None, 3) == N.RS_E_ARG
+    assert N.lib.rs_plan_launch_ceiling(plan.handle, None, 9) == N.RS_E_ARG
+    assert N.lib.rs_plan_launch_ceiling(plan.handle, None, -1) == N.RS_E_ARG
     assert N.lib.rs_plan_launch_ceiling(None, None, 0) == N.RS_E_ARG
     assert N.lib.rs_plan_groups(plan.handle) == max(1, -(-m // 16)) or erase is not None
     assert N.lib.rs_plan_groups(None) == 0
@@ -1371,9 +1375,9 @@ def test_plan_ceiling_modes_then_relaunch(native_lib, k, m, S, batch, erase):
 @pytest.mark.parametrize("k,m,S,batch", [(10, 4, 100_003, 3), (4, 2, 65_537, 5)])
 def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m, S, batch):
     """On an upstream Split-layout batch (misaligned shards, pitch = S) the ceiling modes
-    change nothing but the written shards: the write-only mode stores aligned blocks from
-    each row's first 16-B boundary on, never a byte of a neighbouring input shard; the
-    plan then restores its outputs bit-exactly."""
+    change nothing but the written shards: the write-only modes store aligned blocks from
+    each row's first 16 / 64 / 128 / 256-B boundary on, never a byte of a neighbouring
+    input shard; the plan then restores its outputs bit-exactly."""
     import torch
     from callfs_amd.device import Plan, StripeBatch
     sb = StripeBatch(k, m, S, batch, torch.device("cuda:0"), layout="split")
@@ -1381,7 +1385,7 @@ def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m,
     enc = Plan.for_batch(sb)
     enc.launch()
     before = sb.buf.clone()
-    for mode in ("read", "write", "nolookup"):
+    for mode in ("read", "write", "nolookup", "read128", "write64", "write128", "write256"):
         enc.launch_ceiling(mode)
         torch.cuda.synchronize()
         assert torch.equal(sb.buf[:, :k], before[:, :k]), mode  # inputs untouched

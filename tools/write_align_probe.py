@@ -1,4 +1,4 @@
-"""Write-stream alignment probe (development tool, DESIGN.md §5 Split layout).
+"""Read- and write-stream alignment probe (development tool, DESIGN.md §5 Split layout).
 
 For each shape: the plan's write streams alone (rs_plan_launch_ceiling RS_CEIL_WRITE,
 16-B-aligned rows as the production stores) against the same streams written from each
@@ -35,13 +35,15 @@ def main():
         layout = f[4] if len(f) > 4 else "pitch"
         holder, ptrs = build(k, m, S, B, layout, dev)
         plan = Plan(k, m, S, B, ptrs)
-        modes = ["write", "write64", "write128", "write256"]
+        modes = ["write", "write64", "write128", "write256", "read", "read64", "read128",
+                 "read256"]
         t = {md: [] for md in modes}
         for r in range(a.rounds):
-            for md in modes[r % 4:] + modes[:r % 4]:
+            for md in modes[r % 8:] + modes[:r % 8]:
                 t[md].append(launch_ms(lambda: plan.launch_ceiling(md, stream), stream, a.reps))
-        wb = m * S * B
-        pct = {md: round(wb / (min(x) * 1e-3) / 1e9 / 80.0, 2) for md, x in t.items()}
+        wb, rb = m * S * B, k * S * B
+        pct = {md: round((rb if md.startswith("read") else wb) / (min(x) * 1e-3) / 1e9 / 80.0, 2)
+               for md, x in t.items()}
         print(json.dumps({"shape": spec, "written_bytes": wb, "pct_of_8TBs": pct}), flush=True)
         del plan, holder
         torch.cuda.empty_cache()
