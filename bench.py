@@ -19,7 +19,11 @@ timer.
 
 roofline: the encode kernel's (rs_apply_lds for k >= 4) algorithmic bytes per launch
 ((k+m)*S per stripe) over its average HIP-event duration on the launch stream, against
-8.0 TB/s HBM3E.
+8.0 TB/s HBM3E. The events are recorded by the kernel dispatches themselves
+(rs_plan_launch_timed, hipExtLaunchKernel: start when the plan's first dispatch starts,
+stop when its last ends), i.e. the kernel time rocprofv3's kernel trace reports; the
+stream's gap between one launch and the next is in ms_per_step (and `launch_gap_ms`),
+not in the per-kernel time.
 cpu_baseline: rank 0 at N=1 only — the C port of the reference CPU algorithm
 (oracle/rs_oracle.c orc_bench_codec: upstream GFNI/AVX2 kernels, one native loop,
 stripe-parallel and byte-range threadings, the faster reported) over >= 2 GiB of the
@@ -156,14 +160,15 @@ def cpu_baseline(sb, k, m, erase, seconds, ws_bytes, threads):
 
 
 def _launch_ms(fn, stream, reps=20, warm_ms=30.0):
-    """Mean ms per launch of fn() over `reps` launches, each between two HIP events on
-    `stream`, after >= warm_ms of untimed launches (a kernel timed right after a lighter
-    or heavier one runs off its steady clock for milliseconds)."""
+    """Mean ms per launch of fn(events) over `reps` launches, each timed by a pair of HIP
+    events its kernel dispatches record (as the bench's own launches are), after >=
+    warm_ms of untimed launches (a kernel timed right after a lighter or heavier one runs
+    off its steady clock for milliseconds)."""
     with torch.cuda.stream(stream):
         t0 = time.perf_counter()
         while True:
             for _ in range(4):
-                fn()
+                fn(None)
             torch.cuda.synchronize(stream.device)
             if (time.perf_counter() - t0) * 1e3 >= warm_ms:
                 break
@@ -171,8 +176,9 @@ def _launch_ms(fn, stream, reps=20, warm_ms=30.0):
               for _ in range(reps)]
         for a, b in ev:
             a.record(stream)
-            fn()
             b.record(stream)
+        for pair in ev:
+            fn(pair)
         torch.cuda.synchronize(stream.device)
     return sum(a.elapsed_time(b) for a, b in ev) / reps
 
@@ -186,7 +192,7 @@ def plan_ceilings(enc, dec, stream):
     afterwards (decode first, then encode) so every shard holds its true bytes again."""
     out = {}
     for name, plan in (("decode", dec), ("encode", enc)):
-        ms = {mode: _launch_ms(lambda: plan.launch_ceiling(mode, stream), stream)
+        ms = {mode: _launch_ms(lambda evs: plan.launch_ceiling(mode, stream, events=evs), stream)
               for mode in ("read", "write", "nolookup")}
         plan.corrupt(stream)  # the no-lookup form's Verify rows compare junk: clear
         plan.launch(stream)
@@ -293,7 +299,12 @@ def main(argv=None):
         enc.launch(stream)
         dec.launch(stream)
 
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # per step: encode start / stop, decode start / stop, recorded by the kernel dispatches
+    # (rs_plan_launch_timed); each recorded once here so the HIP events exist
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    for row in ev:
+        for e in row:
+            e.record(stream)
 
     def barrier():
         if world > 1:
@@ -304,11 +315,8 @@ def main(argv=None):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.steps):
-        ev[s][0].record(stream)
-        enc.launch(stream)
-        ev[s][1].record(stream)
-        dec.launch(stream)
-        ev[s][2].record(stream)
+        enc.launch(stream, events=(ev[s][0], ev[s][1]))
+        dec.launch(stream, events=(ev[s][2], ev[s][3]))
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     barrier()
@@ -320,7 +328,7 @@ def main(argv=None):
     elapsed = float(el[0])
 
     enc_all = sorted(e[0].elapsed_time(e[1]) for e in ev)
-    dec_all = sorted(e[1].elapsed_time(e[2]) for e in ev)
+    dec_all = sorted(e[2].elapsed_time(e[3]) for e in ev)
     enc_ms = sum(enc_all) / args.steps
     dec_ms = sum(dec_all) / args.steps
     user_step = 2 * B * k * (S_obj if S_obj else S * world)
@@ -369,6 +377,9 @@ def main(argv=None):
         "decode_gib_s": round(world * B * k * S / (dec_ms * 1e-3) / 2**30, 2),
         "encode_ms": round(enc_ms, 4),
         "decode_ms": round(dec_ms, 4),
+        # wall time per step not inside either plan's kernels: the stream's gaps between
+        # dependent launches (and the host loop, when it falls behind)
+        "launch_gap_ms": round(elapsed * 1e3 / args.steps - enc_ms - dec_ms, 4),
         # median and min per launch beside the mean the roofline uses
         "encode_ms_median_min": [round(enc_all[len(enc_all) // 2], 4), round(enc_all[0], 4)],
         "decode_ms_median_min": [round(dec_all[len(dec_all) // 2], 4), round(dec_all[0], 4)],

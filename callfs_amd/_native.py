@@ -76,11 +76,13 @@ SIGNATURES = {
     "rs_plan_create": (_int, [_vp, _int, _int, _int, _sz, _int, _u8p, ctypes.POINTER(_vp),
                               ctypes.POINTER(_vp)]),
     "rs_plan_launch": (_int, [_vp, _vp]),
+    "rs_plan_launch_timed": (_int, [_vp, _vp, _vp, _vp]),
     "rs_plan_status": (_int, [_vp, _vp, ctypes.POINTER(_int)]),
     "rs_plan_stripe_status": (_int, [_vp, _vp, ctypes.POINTER(_int)]),
     "rs_plan_bytes": (ctypes.c_uint64, [_vp]),
     "rs_plan_groups": (ctypes.c_int, [_vp]),
     "rs_plan_launch_ceiling": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
+    "rs_plan_launch_ceiling_timed": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp, _vp]),
     "rs_plan_destroy": (None, [_vp]),
     "rs_plan_tune": (_int, [_vp, _vp, _int, ctypes.POINTER(_int), _int]),
     "rs_plan_set_orders": (_int, [_vp, ctypes.POINTER(_int), _int]),

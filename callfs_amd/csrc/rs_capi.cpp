@@ -419,13 +419,18 @@ ApplyArgs group_args(const Tables& t, const MetaLayout& L, size_t gi, int batch,
 }
 
 // orders: per launch group, a TileOrder from rs_plan_tune or -1 (the rule); null = rule.
+// ev: the first group's first dispatch records ev.start, the last group's last ev.stop.
 hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_t* d, size_t S,
                          hipStream_t s, int status_stride, const LayoutHint& hint,
-                         const std::vector<int>* orders = nullptr) {
-  for (size_t gi = 0; gi < t.groups.size(); ++gi) {
+                         const std::vector<int>* orders = nullptr, LaunchEvents ev = {}) {
+  const size_t ng = t.groups.size();
+  for (size_t gi = 0; gi < ng; ++gi) {
     const int order = orders && gi < orders->size() ? (*orders)[gi] : -1;
+    LaunchEvents g;
+    g.start = gi == 0 ? ev.start : nullptr;
+    g.stop = gi + 1 == ng ? ev.stop : nullptr;
     hipError_t e = launch_apply(group_args(t, L, gi, batch, d, S, status_stride, hint), s,
-                                /*bytes_only=*/false, order);
+                                /*bytes_only=*/false, order, g);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -1587,6 +1592,10 @@ int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
 }
 
 int rs_plan_launch(rs_plan* plan, void* stream) {
+  return rs_plan_launch_timed(plan, stream, nullptr, nullptr);
+}
+
+int rs_plan_launch_timed(rs_plan* plan, void* stream, void* start_event, void* stop_event) {
   DeviceGuard dg;
   if (!plan) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
@@ -1595,14 +1604,22 @@ int rs_plan_launch(rs_plan* plan, void* stream) {
     std::lock_guard<std::mutex> g(plan->mu);
     orders = plan->orders;
   }
+  LaunchEvents ev;
+  ev.start = static_cast<hipEvent_t>(start_event);
+  ev.stop = static_cast<hipEvent_t>(stop_event);
   HIPCHK(launch_groups(*plan->tables, plan->layout, plan->batch,
                        static_cast<uint8_t*>(plan->dmeta), plan->S,
                        static_cast<hipStream_t>(stream), /*status_stride=*/1, plan->hint,
-                       &orders));
+                       &orders, ev));
   return RS_OK;
 }
 
 int rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode) {
+  return rs_plan_launch_ceiling_timed(plan, stream, mode, nullptr, nullptr);
+}
+
+int rs_plan_launch_ceiling_timed(rs_plan* plan, void* stream, int mode, void* start_event,
+                                 void* stop_event) {
   DeviceGuard dg;
   if (!plan || mode < 0 || mode > 8) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
@@ -1613,10 +1630,14 @@ int rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode) {
   }
   const Tables& t = *plan->tables;
   auto* d = static_cast<uint8_t*>(plan->dmeta);
-  for (size_t gi = 0; gi < t.groups.size(); ++gi) {
+  const size_t ng = t.groups.size();
+  for (size_t gi = 0; gi < ng; ++gi) {
     const int order = gi < orders.size() ? orders[gi] : -1;
+    LaunchEvents ev;
+    ev.start = gi == 0 ? static_cast<hipEvent_t>(start_event) : nullptr;
+    ev.stop = gi + 1 == ng ? static_cast<hipEvent_t>(stop_event) : nullptr;
     HIPCHK(launch_ceiling(group_args(t, plan->layout, gi, plan->batch, d, plan->S, 1, plan->hint),
-                          static_cast<hipStream_t>(stream), order, mode));
+                          static_cast<hipStream_t>(stream), order, mode, ev));
   }
   return RS_OK;
 }

@@ -10,6 +10,8 @@
 #include <type_traits>
 #include <utility>
 
+#include <hip/hip_ext.h>
+
 #include "dispatch.hpp"
 #include "rs_apply.hpp"
 #include "tile_order.hpp"
@@ -139,6 +141,7 @@ uint32_t slice_tiles(int streams) {
 // that only compare (every row a Verify row, no stores) stay whole: read-only streams
 // lose ≈ 1 point to the slice drains and gain nothing (configs[2] shape with nothing
 // erased: 79.0-79.4 % whole vs 78.0-78.4 % sliced).
+// launch(blocks, first, last): first / last = this is the launch's first / last slice.
 template <class Launch>
 void launch_sliced(uint32_t grid, int streams, ApplyArgs& a, Launch&& launch) {
   const uint32_t all_rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
@@ -148,9 +151,21 @@ void launch_sliced(uint32_t grid, int streams, ApplyArgs& a, Launch&& launch) {
   const uint32_t per = (grid + nsl - 1) / nsl;
   for (uint32_t t0 = 0; t0 < grid; t0 += per) {
     a.t_base = t0;
-    launch(std::min(per, grid - t0));
+    launch(std::min(per, grid - t0), t0 == 0, t0 + per >= grid);
   }
   a.t_base = 0;
+}
+
+// One dispatch of kernel fn; with events, the first dispatch of a launch records ev.start
+// at its start and the last records ev.stop at its end (hipExtLaunchKernel).
+template <class... Args>
+void dispatch(void (*fn)(Args...), dim3 grid, dim3 block, size_t lds, hipStream_t stream,
+              const LaunchEvents& ev, bool first, bool last, Args... args) {
+  if (ev.start || ev.stop)
+    hipExtLaunchKernelGGL(fn, grid, block, static_cast<uint32_t>(lds), stream,
+                          first ? ev.start : nullptr, last ? ev.stop : nullptr, 0, args...);
+  else
+    hipLaunchKernelGGL(fn, grid, block, lds, stream, args...);
 }
 constexpr int kLdsMinRows = 5;
 constexpr int kLdsMinK = 4;
@@ -358,7 +373,8 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
   return c;
 }
 
-hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int order) {
+hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int order,
+                        LaunchEvents ev) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
@@ -420,8 +436,10 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           a.tail_in_vec = 1;  // its first tile writes every edge byte, the tail included
           tail0 = a.S;
         }
-        launch_sliced(gx, a.K + a.R, a, [&](uint32_t blocks) {
-          hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, a);
+        const bool tail_after = tail0 < a.S;  // a byte-kernel launch follows: it ends the launch
+        launch_sliced(gx, a.K + a.R, a, [&](uint32_t blocks, bool first, bool last) {
+          dispatch(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, ev, first,
+                   last && !tail_after, a);
         });
       } else {
         a.tail_in_vec = tail0 < a.S;  // as for the LDS kernel: the first tile takes the tail
@@ -436,8 +454,10 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
                           ProdG2Policy::U == ProdPolicy::U && ProdQ16Policy::U == ProdPolicy::U,
                       "one grid shape for every v_perm policy");
         const unsigned gx = dev::vec_grid<ProdPolicy>(a.nvec, a.batch);
-        launch_sliced(gx, a.K + a.R, a, [&](uint32_t blocks) {
-          hipLaunchKernelGGL(fn, dim3(blocks), dim3(ProdPolicy::BS), 0, stream, a);
+        const bool tail_after = tail0 < a.S;
+        launch_sliced(gx, a.K + a.R, a, [&](uint32_t blocks, bool first, bool last) {
+          dispatch(fn, dim3(blocks), dim3(ProdPolicy::BS), 0, stream, ev, first,
+                   last && !tail_after, a);
         });
       }
       hipError_t e = hipGetLastError();
@@ -449,8 +469,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   if (tail0 < a.S) {
     const unsigned gy = static_cast<unsigned>(std::min(a.batch, 65535));
     const uint64_t gx = (a.S - tail0 + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(kByte[a.R - 1], dim3(static_cast<unsigned>(gx), gy), dim3(kBlock), 0,
-                       stream, a, tail0);
+    dispatch(kByte[a.R - 1], dim3(static_cast<unsigned>(gx), gy), dim3(kBlock), 0, stream, ev,
+             /*first=*/a.nvec == 0, /*last=*/true, a, tail0);
     return hipGetLastError();
   }
   return hipSuccess;
@@ -501,7 +521,7 @@ const std::array<VecFn, 3> kStreamReadAligned = {
     &dev::rs_stream_read<0, 64>, &dev::rs_stream_read<0, 128>, &dev::rs_stream_read<0, 256>};
 }  // namespace
 
-hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode) {
+hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, LaunchEvents ev) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1 || !a.ltabs ||
       mode < 0 || mode > 8)
     return hipErrorInvalidValue;
@@ -524,8 +544,8 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode) 
                      : mode >= 3 ? kStreamWriteAligned[mode - 3]
                                : (mode == 1 ? kStreamRead : kStreamWrite)[static_cast<int>(ord)];
     a.tail_in_vec = 0;
-    launch_sliced(grid, a.K + a.R, a, [&](uint32_t blocks) {
-      hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), 0, stream, a);
+    launch_sliced(grid, a.K + a.R, a, [&](uint32_t blocks, bool first, bool last) {
+      dispatch(fn, dim3(blocks), dim3(LdsPolicy::BS), 0, stream, ev, first, last, a);
     });
     return hipGetLastError();
   }
@@ -538,8 +558,8 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode) 
   if (lds > (64u << 10))
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
-  launch_sliced(grid, a.K + a.R, a, [&](uint32_t blocks) {
-    hipLaunchKernelGGL(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, a);
+  launch_sliced(grid, a.K + a.R, a, [&](uint32_t blocks, bool first, bool last) {
+    dispatch(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, ev, first, last, a);
   });
   return hipGetLastError();
 }

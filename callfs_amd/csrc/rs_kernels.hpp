@@ -109,7 +109,15 @@ constexpr int kOrderRealign = 32;
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the
 // rule (or CALLFS_RS_TILE_ORDER).
-hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false, int order = -1);
+// ev_start / ev_stop (optional, created by the caller): recorded by the launch's first
+// kernel dispatch when it starts and by its last when it ends (hipExtLaunchKernel), so
+// their interval is the kernels' own time without the stream's gaps before and after.
+struct LaunchEvents {
+  hipEvent_t start = nullptr;
+  hipEvent_t stop = nullptr;
+};
+hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false, int order = -1,
+                        LaunchEvents ev = {});
 
 // Tile orders worth timing for launch `a` (rs_plan_tune): the rule's choice first, then
 // the alternatives that have kernel instances for this path. Empty when the launch has
@@ -124,7 +132,8 @@ std::vector<int> order_candidates(const ApplyArgs& a, bool every_instance = fals
 //           flag status);
 //   mode 1  the launch's read streams alone (inputs + Verify rows; writes nothing);
 //   mode 2  its write streams alone (junk into the written rows).
-hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode);
+hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode,
+                          LaunchEvents ev = {});
 
 
 // Tuning hook for tools/kbench.hip (not part of the C ABI): tiles per launch slice for

@@ -100,21 +100,41 @@ class Plan:
         """Algorithmic HBM bytes one launch moves."""
         return int(N.lib.rs_plan_bytes(self.handle))
 
-    def launch(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+    def launch(self, stream: Optional[torch.cuda.Stream] = None, events=None) -> None:
+        """rs_plan_launch; events = (start, stop) torch.cuda.Event pair (timing enabled,
+        recorded at least once so the HIP events exist): rs_plan_launch_timed, the
+        first kernel dispatch records start when it starts and the last records stop when
+        it ends, so start.elapsed_time(stop) is the kernels' own time."""
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        N.check(N.lib.rs_plan_launch(self.handle, ctypes.c_void_p(s.cuda_stream)), "rs_plan_launch")
+        if events is None:
+            N.check(N.lib.rs_plan_launch(self.handle, ctypes.c_void_p(s.cuda_stream)),
+                    "rs_plan_launch")
+            return
+        h = [ctypes.c_void_p(e.cuda_event) for e in events]
+        if not all(x.value for x in h):
+            raise ValueError("record each event once before timing launches with it")
+        N.check(N.lib.rs_plan_launch_timed(self.handle, ctypes.c_void_p(s.cuda_stream), *h),
+                "rs_plan_launch_timed")
 
     CEILINGS = {"nolookup": 0, "read": 1, "write": 2, "write64": 3, "write128": 4,
                 "write256": 5, "read64": 6, "read128": 7, "read256": 8}
 
     def launch_ceiling(self, mode: str = "nolookup",
-                       stream: Optional[torch.cuda.Stream] = None) -> None:
+                       stream: Optional[torch.cuda.Stream] = None, events=None) -> None:
         """rs_plan_launch_ceiling (measurement only): this plan's traffic as the kernel's
         no-lookup form, or its read / write streams alone, same grid and tile order.
-        "nolookup" and "write" leave junk in the written shards."""
+        "nolookup" and "write" leave junk in the written shards. events: as for launch()."""
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        N.check(N.lib.rs_plan_launch_ceiling(self.handle, ctypes.c_void_p(s.cuda_stream),
-                                             self.CEILINGS[mode]), "rs_plan_launch_ceiling")
+        if events is None:
+            N.check(N.lib.rs_plan_launch_ceiling(self.handle, ctypes.c_void_p(s.cuda_stream),
+                                                 self.CEILINGS[mode]), "rs_plan_launch_ceiling")
+            return
+        h = [ctypes.c_void_p(e.cuda_event) for e in events]
+        if not all(x.value for x in h):
+            raise ValueError("record each event once before timing launches with it")
+        N.check(N.lib.rs_plan_launch_ceiling_timed(self.handle, ctypes.c_void_p(s.cuda_stream),
+                                                   self.CEILINGS[mode], *h),
+                "rs_plan_launch_ceiling_timed")
 
     # tile orders (RS_ORDER_*); on misaligned shards 0..6 name the plain kernel with
     # unaligned accesses and "realign*" the kernel that aligns loads and stores

@@ -158,6 +158,13 @@ int  rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
 int  rs_plan_launch(rs_plan* plan, void* stream);
 int  rs_plan_status(rs_plan* plan, void* stream, int* corrupt);
 int  rs_plan_stripe_status(rs_plan* plan, void* stream, int* flags);
+/* rs_plan_launch that also times its kernels (measurement; no upstream counterpart):
+ * start_event / stop_event (hipEvent_t, created by the caller, either may be NULL) are
+ * recorded by the launch's first kernel dispatch when it starts and by its last when it
+ * ends (hipExtLaunchKernel), so hipEventElapsedTime gives the kernels' own time, without
+ * the stream's gap before the first and after the last (what rocprofv3's kernel trace
+ * reports). */
+int  rs_plan_launch_timed(rs_plan* plan, void* stream, void* start_event, void* stop_event);
 uint64_t rs_plan_bytes(const rs_plan* plan);
 void rs_plan_destroy(rs_plan* plan);
 
@@ -213,6 +220,9 @@ int  rs_plan_set_orders(rs_plan* plan, const int* orders, int n);
 #define RS_CEIL_READ_AL128 7
 #define RS_CEIL_READ_AL256 8
 int  rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode);
+/* The same, with its kernels timed as rs_plan_launch_timed times the plan's. */
+int  rs_plan_launch_ceiling_timed(rs_plan* plan, void* stream, int mode, void* start_event,
+                                  void* stop_event);
 /* Launch groups of a plan (the `orders` entries rs_plan_tune can fill): one per up to 16
  * written or compared rows; 0 for a NULL plan. */
 int  rs_plan_groups(const rs_plan* plan);

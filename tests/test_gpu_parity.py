@@ -1372,6 +1372,47 @@ def test_plan_ceiling_modes_then_relaunch(native_lib, k, m, S, batch, erase):
     assert N.lib.rs_plan_groups(None) == 0
 
 
+@pytest.mark.parametrize("k,m,S,batch,erase", [
+    (10, 4, 1 << 20, 8, None),      # one LDS dispatch
+    (20, 20, 65_536, 4, None),      # two launch groups: start on the first, stop on the last
+    (4, 2, 10, 3, (0,)),            # S < 16: the byte kernel alone
+])
+def test_plan_launch_timed_events(native_lib, k, m, S, batch, erase):
+    """rs_plan_launch_timed: the plan's first kernel dispatch records the start event and
+    its last the stop event; the interval is positive and no longer than the same launch
+    bracketed by stream events; outputs stay bit-exact. The ceiling modes time the same
+    way. Events that do not exist yet are refused by the Python wrapper."""
+    import torch
+    from callfs_amd.device import Plan
+    sb = _batch(k, m, S, batch, seed=S + 11 * k)
+    present = None if erase is None else [i not in erase for i in range(k + m)]
+    enc = Plan.for_batch(sb)
+    plan = enc if erase is None else Plan.for_batch(sb, present=present)
+    enc.launch()
+    want = sb.buf.clone()
+    stream = torch.cuda.current_stream()
+    a, b, c, d = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+    with pytest.raises(ValueError):
+        plan.launch(stream, events=(a, b))
+    for e in (a, b, c, d):
+        e.record(stream)
+    for _ in range(3):
+        if erase is not None:
+            sb.buf[:, list(erase)].zero_()
+        c.record(stream)
+        plan.launch(stream, events=(a, b))
+        d.record(stream)
+        torch.cuda.synchronize()
+        kern, outer = a.elapsed_time(b), c.elapsed_time(d)
+        assert 0 < kern <= outer * 1.02 + 0.005, (kern, outer)
+    assert not plan.corrupt()
+    assert torch.equal(sb.buf[:, :, :S], want[:, :, :S])
+    if S >= 16:
+        plan.launch_ceiling("read", stream, events=(a, b))
+        torch.cuda.synchronize()
+        assert a.elapsed_time(b) > 0
+
+
 @pytest.mark.parametrize("k,m,S,batch", [(10, 4, 100_003, 3), (4, 2, 65_537, 5)])
 def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m, S, batch):
     """On an upstream Split-layout batch (misaligned shards, pitch = S) the ceiling modes
