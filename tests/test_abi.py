@@ -78,6 +78,22 @@ def test_profile_errors_without_device(native_lib):
     assert native_lib.lib.rs_shard_size(200, 57, 10, ctypes.byref(ss)) == native_lib.RS_E_UNSUPPORTED
 
 
+def test_plan_entry_points_refuse_null_plans(native_lib):
+    """The device-plan entry points check their arguments before touching a device:
+    NULL plans (and bad counts / modes) return RS_E_ARG on a host with no GPU."""
+    L = native_lib.lib
+    E = native_lib.RS_E_ARG
+    orders = (ctypes.c_int * 2)(0, -1)
+    assert L.rs_plan_set_orders(None, orders, 2) == E
+    assert L.rs_plan_set_orders(None, None, 0) == E
+    assert L.rs_plan_launch(None, None) == E
+    assert L.rs_plan_launch_timed(None, None, None, None) == E
+    assert L.rs_plan_launch_ceiling(None, None, 0) == E
+    assert L.rs_plan_launch_ceiling_timed(None, None, 1, None, None) == E
+    assert L.rs_plan_tune(None, None, 1, None, 0) == E
+    assert L.rs_plan_groups(None) == 0
+
+
 def test_init_fails_loudly_without_gpu(native_lib):
     import torch
     if torch.cuda.is_available():
