@@ -278,7 +278,8 @@ TileOrder lds_rule(const ApplyArgs& a) {
   if (forced >= 0) return static_cast<TileOrder>(forced);
   const uint32_t rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
   return lds_tile_order(a.S, (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS, a.addr_tz, a.K + a.R,
-                        a.stripe_stride, (a.verify_mask & rows) != 0);
+                        a.stripe_stride, (a.verify_mask & rows) != 0,
+                        (a.verify_mask & rows) == rows);
 }
 
 TileOrder wide_rule(const ApplyArgs& a) {
@@ -360,7 +361,8 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(TileOrder::kSeg8);
       add(TileOrder::kSeg16);
     }
-    if (every_instance) {  // never faster than the rule's order on aligned shards
+    if (every_instance) {  // on aligned shards never faster than the rule's order, which
+                           // is X32 itself for read-only launches
       add(TileOrder::kXcd8);
       add(TileOrder::kXcd32);
     }

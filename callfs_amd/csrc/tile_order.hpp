@@ -46,14 +46,13 @@ CALLFS_HD inline void map_tile(uint32_t t, uint32_t tps, uint32_t batch, uint32_
 
 // XCD-grouped consecutive orders (ORD 10: X8, 11: X32). A dispatch deals its blocks to the
 // 8 XCDs round-robin (block b of the launch runs on XCD b % 8), so in consecutive order
-// the two tiles on either side of every tile boundary of a row run on different XCDs,
-// each with its own L2. Where a row's tile boundaries fall inside a 64-B line (rows at a
-// 16-B-granular pitch, the Split layout), each L2 then writes its part of that line back
-// as a partial write. X8 / X32 give the blocks b, b+8, b+16, ... of every group of 8*J
-// blocks J consecutive tiles (J = 8 / 32), so the tiles in flight are those of
-// consecutive order, permuted within the group, and only one boundary in J crosses XCDs.
-// Blocks past the last full group keep their place. Host-side as well: host_test checks
-// that the map is a bijection.
+// neighbouring tiles of a row run on different XCDs, each with its own L2. X8 / X32 give
+// the blocks b, b+8, b+16, ... of every group of 8*J blocks J consecutive tiles (J = 8 /
+// 32): the tiles in flight are those of consecutive order, permuted within the group, and
+// each XCD streams runs of J neighbouring tiles. Measured: write streams
+// unchanged, read streams of 6.7 MB shards 6 % shorter; adopted for the realigning kernel
+// and for read-only launches (lds_tile_order). Blocks past the last full group keep their
+// place. Host-side as well: host_test checks that the map is a bijection.
 template <int ORD>
 CALLFS_HD inline uint32_t block_tile(uint32_t b, uint32_t nblocks) {
   if constexpr (ORD >= 10) {
@@ -96,10 +95,21 @@ constexpr int kTileOrders = 7;
 // 75.9, nothing erased 77.4 -> 78.1; tools/ceiling_sweep.py, profiles/r03/ceil1,
 // profiles/r02/decode_order_sweep).
 //
+// Launch groups that only compare (every row a Verify row: the download with nothing
+// lost, codec.go:59, read-only) take X32 above 256 KiB shards: tools/order_ab.py,
+// profiles/r03/dec3, dec4 (three runs, two boxes), % of 8 TB/s, rule -> X32: RS(10,4)
+// 1 MiB 85.0 / 85.4 / 85.1 -> 85.8 / 86.4 / 85.5, 6.7 MB 83.3 / 84.4 / 83.2 -> 84.0 /
+// 84.0 / 84.5, RS(4,2) 1 MiB 82.3 / 82.3 -> 82.9 / 83.5, RS(16,4) 4 MiB 80.2 / 80.3 ->
+// 81.2 / 81.4, RS(6,3) 2.8 MB 84.8 / 84.6 -> 85.3 / 85.3; at 105 KB shards all orders
+// within 0.3.
+//
 // tps = tiles of 512 16-B vectors (8 KiB) per stripe; streams = K + R of the launch;
-// addr_tz / stripe_stride as in ApplyArgs; verify = the launch compares some rows.
+// addr_tz / stripe_stride as in ApplyArgs; verify = the launch compares some rows,
+// read_only = it compares every row (writes nothing).
 inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int streams,
-                                uint64_t stripe_stride, bool verify = false) {
+                                uint64_t stripe_stride, bool verify = false,
+                                bool read_only = false) {
+  if (read_only && tps > 32) return TileOrder::kXcd32;
   // stripes exactly 2 MiB apart: interleaving stripes costs 2-12 points (RS(8,8) 128 KiB
   // 72.4 -> 60.6 with G8, RS(4,4) 256 KiB 77.9 -> 65.8, RS(6,2) 256 KiB 81.5 -> 78.4);
   // strides of 1, 4, 8 or 16 MiB interleave fine (profiles/r01/tile_order/segments/

@@ -264,6 +264,10 @@ int main() {
     // decodes with Verify rows: consecutive from 1 to 8 MiB, G2 up to 1 MiB
     CHECK(lds_tile_order(6710887, tps_of(6710887), 8, 14, 14 * 6711040ull, true) == TileOrder::kConsecutive);
     CHECK(lds_tile_order(MiB, tps_of(MiB), 20, 14, 14 * MiB, true) == TileOrder::kGroup2);
+    // read-only (every row compared: the download with nothing lost) above 256 KiB: X32
+    CHECK(lds_tile_order(MiB, tps_of(MiB), 20, 14, 14 * MiB, true, true) == TileOrder::kXcd32);
+    CHECK(lds_tile_order(6710887, tps_of(6710887), 8, 14, 14 * 6711040ull, true, true) == TileOrder::kXcd32);
+    CHECK(lds_tile_order(104858, tps_of(104858), 8, 14, 14 * 105216ull, true, true) == TileOrder::kGroup8);
     // RS(4,2) 4 MiB: consecutive (few streams); RS(16,4) 4 MiB: G2
     CHECK(lds_tile_order(4 * MiB, tps_of(4 * MiB), 22, 6, 24 * MiB) == TileOrder::kConsecutive);
     CHECK(lds_tile_order(4 * MiB, tps_of(4 * MiB), 22, 20, 80 * MiB) == TileOrder::kGroup2);
