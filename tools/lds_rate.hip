@@ -78,6 +78,70 @@ __global__ __launch_bounds__(512) void lds_rate(const uint32_t* seed, uint32_t* 
   if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[0] = 1;
 }
 
+// Wider-index variant (round 3 probe): 2^B-entry tables of W bytes (B = 5 with W = 8, B = 6
+// with W = 4: 256 B per table, so every entry still owns its banks), each lookup resolving
+// B input bits. The index of each lookup is assembled from two data words the way a
+// piece spanning two shards would be (two shifts and one three-input op per 4 lookups).
+template <int W, int B>
+__global__ __launch_bounds__(512) void lds_rate_wide(const uint32_t* seed, uint32_t* out, int iters) {
+  __shared__ __attribute__((aligned(256))) uint8_t tab[32 * 16 * 16];
+  for (int j = threadIdx.x; j < 32 * 16 * 16 / 4; j += 512)
+    reinterpret_cast<uint32_t*>(tab)[j] = j * 2654435761u;
+  __syncthreads();
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)tab));
+  uint32_t x[4];
+  for (int w = 0; w < 4; ++w) x[w] = seed[(blockIdx.x * 512 + threadIdx.x) * 4 + w];
+  u32x2 acc = {0, 0};
+  constexpr uint32_t kMask = (((1u << B) - 1u) * W) * 0x01010101u;  // idx*W in each byte
+  static_assert(((1 << B) - 1) * W < 256, "entry offset must fit a byte");
+  for (int it = 0; it < iters; ++it) {
+    const uint32_t base = lds0 + static_cast<uint32_t>(it & 15) * 512u;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        // piece word: low bits from x[w], high bits from x[w+1] (a piece across two shards)
+        const uint32_t lo = x[w] >> (h ? 3 : 1), hi = x[(w + 1) & 3] << (h ? 5 : 2);
+        const uint32_t p = (lo & kMask) ^ (hi & kMask & 0xE0E0E0E0u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t sel = 0x07060500u | static_cast<uint32_t>(j);
+          const uint32_t a = __builtin_amdgcn_perm(base + 256u * h, p, sel);
+          if constexpr (W == 8) {
+            acc ^= *(const __attribute__((address_space(3))) u32x2*)(static_cast<uintptr_t>(a));
+          } else {
+            acc.x ^= *(const __attribute__((address_space(3))) uint32_t*)(static_cast<uintptr_t>(a));
+          }
+        }
+      }
+      x[w] = x[w] * 1664525u + 1013904223u;
+    }
+  }
+  if ((acc.x ^ acc.y) == 0x12345678u) out[0] = 1;
+}
+
+template <int W, int B>
+void run_wide(const uint32_t* seed, uint32_t* out, int blocks, int iters, size_t dyn) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL((lds_rate_wide<W, B>), dim3(blocks), dim3(512), dyn, 0, seed, out, iters);
+  CK(hipGetLastError());
+  CK(hipEventRecord(a));
+  const int reps = 5;
+  for (int rep = 0; rep < reps; ++rep) hipLaunchKernelGGL((lds_rate_wide<W, B>), dim3(blocks), dim3(512), dyn, 0, seed, out, iters);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  const double lookups = static_cast<double>(blocks) * 512 * iters * 32 * reps;
+  const double s = ms * 1e-3;
+  std::printf("{\"W\": %d, \"index_bits\": %d, \"waves_per_simd\": %d, \"lookups_per_s\": %.4g, \"lds_TBps\": %.2f, "
+              "\"data_bytes_per_s_TB\": %.2f}\n",
+              W, B, dyn ? static_cast<int>(8 * ((160u << 10) / (dyn + 8192)) / 4) : 8, lookups / s, lookups * W / s / 1e12,
+              lookups * B / 8.0 / s / 1e12);
+}
+
 template <int W>
 void run(const uint32_t* seed, uint32_t* out, int blocks, int iters, double ghz, size_t dyn) {
   hipEvent_t a, b;
@@ -122,6 +186,12 @@ int main(int argc, char** argv) {
     run<4>(seed, out, blocks, iters, ghz, dyn);
     run<8>(seed, out, blocks, iters, ghz, dyn);
     run<16>(seed, out, blocks, iters, ghz, dyn);
+    if (dyn) {
+      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate_wide<8, 5>), hipFuncAttributeMaxDynamicSharedMemorySize, (160 << 10) - 8192));
+      CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_rate_wide<4, 6>), hipFuncAttributeMaxDynamicSharedMemorySize, (160 << 10) - 8192));
+    }
+    run_wide<8, 5>(seed, out, blocks, iters, dyn);
+    run_wide<4, 6>(seed, out, blocks, iters, dyn);
   }
   return 0;
 }
