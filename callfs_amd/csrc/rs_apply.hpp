@@ -104,8 +104,14 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //            global_load_dwordx4
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
           int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, int REALIGN_ = 0,
-          bool SDWA_ = false, int PROBE_ = 0, int VPF_ = 0>
+          bool SDWA_ = false, int PROBE_ = 0, int VPF_ = 0, bool WIX_ = false>
 struct Policy {
+  // LDS kernel, R <= 4, plain ring-of-three loop: input shards in triples, each byte
+  // position of a triple resolved by four 6-bit lookups into 64-entry tables of 4-byte
+  // entries (built in LDS from the nibble tables) instead of six nibble lookups
+  static constexpr bool WIX = WIX_;
+  static_assert(!WIX_ || (REALIGN_ == 0 && RING_ == 0 && VPF_ == 0 && !NOMATH_ && !SDWA_),
+                "WIX: plain ring-of-three encode kernel only");
   // > 0: Verify rows' stored vectors are loaded VPF shards before the end of the input
   // loop instead of after it (R <= 4, plain loads, ring of three only)
   static constexpr int VPF = VPF_;
@@ -528,6 +534,59 @@ __device__ __forceinline__ void lds_mac(typename LdsAcc<RT>::T (&acc)[4][4], con
   }
 }
 
+// ---- 6-bit lookups over shard triples (Policy::WIX, R <= 4) ---------------------------
+// Three shards A, B, C give 24 bits per byte position; four 6-bit pieces cover them:
+// P0 = A[5:0], P1 = A[7:6] | B[3:0] << 2, P2 = B[7:4] | C[1:0] << 4, P3 = C[7:2]. Each piece
+// indexes a 64-entry table of 4-byte entries (the R <= 4 row products of its bits), 256 B,
+// so every entry still owns its bank and the lookups never conflict. Per byte position of
+// a triple: 4 lookups instead of 6 nibble lookups, 2 XOR3 instead of 3.
+// LDS layout: the nibble tables (K * 32 * 8 B) first, then per triple g four tables at
+// wix_base(K) + 1024 g + 256 t; entries are built from the nibble tables after they land.
+__host__ __device__ inline uint32_t wix_base(int K) { return static_cast<uint32_t>(K) * 256u; }
+inline size_t lds_bytes_wix(int K) { return static_cast<size_t>(K) * 256 + static_cast<size_t>(K / 3) * 1024; }
+
+// Entry e of table t of triple g from the nibble tables at lds0 (low table of shard i at
+// 256 i + 8 n, high at 256 i + 128 + 8 n; the first 4 bytes hold rows 0..3).
+__device__ __forceinline__ uint32_t wix_entry(uint32_t lds0, uint32_t g, uint32_t t, uint32_t e) {
+  const uint32_t A = lds0 + 768u * g, B = A + 256u, C = B + 256u;
+  uint32_t p, q;
+  switch (t) {
+    case 0: p = A + 8u * (e & 15u); q = A + 128u + 8u * (e >> 4); break;
+    case 1: p = A + 128u + 8u * ((e & 3u) << 2); q = B + 8u * (e >> 2); break;
+    case 2: p = B + 128u + 8u * (e & 15u); q = C + 8u * (e >> 4); break;
+    default: p = C + 8u * ((e & 3u) << 2); q = C + 128u + 8u * (e >> 2); break;
+  }
+  return *(lds_ptr<uint32_t>)(static_cast<uintptr_t>(p)) ^ *(lds_ptr<uint32_t>)(static_cast<uintptr_t>(q));
+}
+
+// acc[w][j] ^= products of byte j of dword w of shards a, b, c (tables at `base`, 256-B
+// aligned: v_perm drops the scaled piece into its low byte).
+template <int RT>
+__device__ __forceinline__ void wix_mac(uint32_t (&acc)[4][4], const uint4& a, const uint4& b,
+                                        const uint4& c, uint32_t base) {
+  static_assert(RT <= 4, "4-byte entries");
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t aw = word(a, w), bw = word(b, w), cw = word(c, w);
+    // piece * 4 in every byte
+    const uint32_t q0 = (aw << 2) & 0xfcfcfcfcu;
+    const uint32_t q1 = ((aw >> 4) & 0x0c0c0c0cu) | ((bw << 4) & 0xf0f0f0f0u);
+    const uint32_t q2 = ((bw >> 2) & 0x3c3c3c3cu) | ((cw << 6) & 0xc0c0c0c0u);
+    const uint32_t q3 = cw & 0xfcfcfcfcu;
+    uint32_t l[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t sel = 0x07060500u | static_cast<uint32_t>(j);
+      l[j][0] = *(lds_ptr<uint32_t>)(static_cast<uintptr_t>(__builtin_amdgcn_perm(base, q0, sel)));
+      l[j][1] = *(lds_ptr<uint32_t>)(static_cast<uintptr_t>(__builtin_amdgcn_perm(base + 256u, q1, sel)));
+      l[j][2] = *(lds_ptr<uint32_t>)(static_cast<uintptr_t>(__builtin_amdgcn_perm(base + 512u, q2, sel)));
+      l[j][3] = *(lds_ptr<uint32_t>)(static_cast<uintptr_t>(__builtin_amdgcn_perm(base + 768u, q3, sel)));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[w][j] = xor3(xor3(acc[w][j], l[j][0], l[j][1]), l[j][2], l[j][3]);
+  }
+}
+
 // Row r's word = byte r of T[0..3].
 template <int RT>
 __device__ __forceinline__ uint32_t lds_row(const typename LdsAcc<RT>::T (&t)[4], int r) {
@@ -664,6 +723,15 @@ void rs_apply_lds(ApplyArgs a) {
     for (int j = threadIdx.x; j < K * 2 * W; j += BS) dst[j] = src[j];
   }
   __syncthreads();
+  if constexpr (P::WIX) {  // the triples' 6-bit tables, from the nibble tables
+    const uint32_t l0 = static_cast<uint32_t>(
+        reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)smem));
+    const uint32_t n = static_cast<uint32_t>(K / 3) * 256u;
+    for (uint32_t j = threadIdx.x; j < n; j += BS)
+      *(__attribute__((address_space(3))) uint32_t*)(static_cast<uintptr_t>(l0 + wix_base(K) + 4u * j)) =
+          wix_entry(l0, j >> 8, (j >> 6) & 3u, j & 63u);
+    __syncthreads();
+  }
   // absolute LDS address of the tables (0 unless static LDS is ever added)
   const uint32_t lds0 = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)smem));
@@ -720,6 +788,23 @@ void rs_apply_lds(ApplyArgs a) {
         x0 = x1;
         x1 = x2;
       }
+    } else if constexpr (P::WIX) {
+      // triples: the next triple's three loads are in flight while one is consumed; the
+      // K % 3 shards left over take the nibble tables
+      const int KT = K / 3;
+      uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = K > 2 ? ld(2) : x0;
+#pragma unroll 1
+      for (int g = 0; g < KT; ++g) {
+        const int i = 3 * g + 3;
+        const uint4 n0 = i < K ? ld(i) : x0, n1 = i + 1 < K ? ld(i + 1) : x0,
+                    n2 = i + 2 < K ? ld(i + 2) : x0;
+        wix_mac<RT>(acc, x0, x1, x2, lds0 + wix_base(K) + 1024u * static_cast<uint32_t>(g));
+        x0 = n0;
+        x1 = n1;
+        x2 = n2;
+      }
+      if (3 * KT < K) lds_mac<RT>(acc, x0, lds0 + static_cast<uint32_t>(3 * KT) * 32u * W);
+      if (3 * KT + 1 < K) lds_mac<RT>(acc, x1, lds0 + static_cast<uint32_t>(3 * KT + 1) * 32u * W);
     } else if constexpr (P::RING == 0) {
       // ring of three shard vectors: shard i is consumed while i+1, i+2 load
       uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = x0;

@@ -83,6 +83,10 @@ using LdsVerifyPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, fal
 // 68.9 realigned, so rs_plan_tune offers the unaligned kernel as an alternative.
 // (R <= 4 asks for 8 waves per SIMD: left alone the compiler used 106 SGPRs, 7 waves)
 // One instance per tile order it runs in: consecutive, X8, X32 (tile_order.hpp block_tile).
+// R <= 4 with 6-bit lookups over shard triples (rs_apply.hpp Policy::WIX): 4 lookups per
+// byte position of three shards instead of 6; one instance per tile order.
+template <int ORD>
+using LdsWixPolicy = dev::Policy<8, 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, true>;
 template <int ORD>
 using LdsRealignOutPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 2>;
 template <int ORD>
@@ -217,6 +221,15 @@ const std::array<std::array<VecFn, 4>, kTileOrders> kLdsVerify = {
     lds_order_table<LdsVerifyPolicy<8>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsVerifyPolicy<10>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsVerifyPolicy<11>>(std::make_integer_sequence<int, 4>{})};
+// [tile order][R - 1] for R <= 4, 6-bit triple lookups
+const std::array<std::array<VecFn, 4>, kTileOrders> kLdsWix = {
+    lds_order_table<LdsWixPolicy<0>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsWixPolicy<2>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsWixPolicy<5>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsWixPolicy<6>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsWixPolicy<8>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsWixPolicy<10>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsWixPolicy<11>>(std::make_integer_sequence<int, 4>{})};
 template <int ORD, int... Rs>
 constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1, ORD>>...};
@@ -309,6 +322,28 @@ bool takes_lds(const ApplyArgs& a) { return a.R >= kLdsMinRows || a.K >= kLdsMin
 bool can_realign(const ApplyArgs& a) {
   return a.R <= 8 && (a.in_misalign || a.out_misalign) && realign_out_enabled();
 }
+// 6-bit triple lookups (Policy::WIX): R <= 4, K >= 3, aligned shards, no Verify rows
+bool can_wix(const ApplyArgs& a) {
+  const uint32_t rows = (1u << a.R) - 1;
+  return a.R <= 4 && a.K >= 3 && !(a.in_misalign | a.out_misalign) && !(a.verify_mask & rows);
+}
+// CALLFS_RS_WIX=0 keeps every launch on the nibble kernel (A/B)
+bool wix_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CALLFS_RS_WIX");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+// The rule takes it for 4 <= K <= 8 (K = 3 runs the v_perm kernel), in the nibble rule's
+// tile order. tools/wix_ab*.sh, profiles/r03/wix/, % of 8 TB/s, best nibble order -> WIX
+// in the rule's order, one box: RS(4,2) 1 MiB 72.3 -> 79.0-79.6 (4 MiB 71.4 -> 78.6, 1 MiB
+// objects 71.4 -> 77.4), RS(4,4) 75.0 -> 81.5, RS(5,2) 73.3 -> 78.9, RS(5,3) 74.5 -> 79.9,
+// RS(6,2) 74.6 -> 77.5, RS(6,3) 74.1 -> 75.5, RS(7,3) 75.1 -> 77.3, RS(8,2) 74.9 -> 77.7,
+// RS(8,4) 76.5 -> 80.1 (128 KiB shards: equal); from K = 9 on equal or slower (RS(9,4) and
+// RS(10,4) equal, RS(12,3) -1.5, RS(16,4) -1.5, RS(20,4) -1.2, RS(32,4) -1.4), where
+// rs_plan_tune still times it for K <= 12.
+bool takes_wix(const ApplyArgs& a) { return can_wix(a) && a.K <= 8 && wix_enabled(); }
 bool takes_realign(const ApplyArgs& a) {
   return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u);
 }
@@ -347,7 +382,11 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
     const auto realign_in = [](TileOrder o) {
       return static_cast<TileOrder>(kOrderRealign + static_cast<int>(o));
     };
+    const auto wix_in = [](TileOrder o) {
+      return static_cast<TileOrder>(kOrderWix + static_cast<int>(o));
+    };
     if (takes_realign(a)) add(realign_in(TileOrder::kXcd32));
+    if (takes_wix(a)) add(wix_in(lds_rule(a)));  // the rule's kernel first
     add(lds_rule(a));
     if (can_realign(a)) {
       add(realign_in(TileOrder::kXcd32));
@@ -366,6 +405,12 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(TileOrder::kXcd8);
       add(TileOrder::kXcd32);
     }
+    if (can_wix(a) && (every_instance || (a.K <= 12 && wix_enabled()))) {
+      // timed up to K = 12 (equal at 9..10 on one box, -1.5 at 12); every instance on request
+      const int n0 = static_cast<int>(c.size());
+      for (int i = 0; i < n0; ++i)
+        if (c[i] >= 0 && c[i] < kTileOrders) add(wix_in(static_cast<TileOrder>(c[i])));
+    }
     return c;
   }
   add(vec_rule(a));
@@ -380,6 +425,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
+  const bool wix = order >= kOrderWix ? can_wix(a) : order < 0 && takes_wix(a);
+  if (order >= kOrderWix) order -= kOrderWix;
   uint64_t tail0 = 0;
   a.tail_in_vec = 0;
   if (!bytes_only) {
@@ -392,7 +439,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         a.tail_in_vec = tail0 < a.S;
         if (a.tail_in_vec) tail0 = a.S;
         if (!a.ltabs) return hipErrorInvalidValue;
-        const size_t lds = dev::lds_bytes(a.K, a.R);
+        size_t lds = dev::lds_bytes(a.K, a.R);
         VecFn fn = kLds[a.R - 1];
         if (a.R <= 8) {  // (8-byte entries: at most 64 KiB of tables, no opt-in needed)
           const TileOrder ord =
@@ -410,6 +457,10 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           const int oi = static_cast<int>(ord);
           if (a.R <= 4 && (a.verify_mask & rows) && oi >= 0 && oi < kTileOrders)
             fn = kLdsVerify[oi][a.R - 1];
+          if (wix && oi >= 0 && oi < kTileOrders) {  // (at most 42 KiB of tables at K = 128)
+            fn = kLdsWix[oi][a.R - 1];
+            lds = dev::lds_bytes_wix(a.K);
+          }
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }
@@ -530,6 +581,7 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
   a.tail_in_vec = a.nvec * 16 < a.S;
+  if (order >= kOrderWix) order -= kOrderWix;  // bounded by the nibble kernel's traffic
   // the order the production launch would take (a tuned order, else the rule; the
   // realigning and v_perm launches are bounded by the plain kernel's traffic)
   static constexpr TileOrder kRealignOrders[3] = {TileOrder::kConsecutive, TileOrder::kXcd8,

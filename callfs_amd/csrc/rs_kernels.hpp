@@ -105,6 +105,9 @@ inline int shard_addr_tz(const void* const* p, int count) {
 // kernel with unaligned accesses)
 // (kOrderRealign + the TileOrder it runs in: consecutive, X8 or X32)
 constexpr int kOrderRealign = 32;
+// (kOrderWix + a TileOrder: the R <= 4 LDS kernel with 6-bit lookups over shard triples,
+// rs_apply.hpp Policy::WIX; aligned launches without Verify rows, K >= 3)
+constexpr int kOrderWix = 64;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the

@@ -1179,7 +1179,11 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
     enc = Plan.for_batch(sb)
     names = enc.tune(reps=1)
     assert len(names) == max(1, -(-m // 16))
-    assert all(n in {"consecutive", "g8", "g2", "q8", "q16", "x8", "x32"} for n in names), names
+    plain = {"consecutive", "g8", "g2", "q8", "q16", "x8", "x32"}
+    # an encode plan with R <= 4 rows may also take the 6-bit triple lookups (K <= 12)
+    wix_ok = 4 <= k <= 12 and m <= 4
+    allowed = plain | ({"wix-" + o for o in plain} | {"wix"} if wix_ok else set())
+    assert all(n in allowed for n in names), names
     sb.fill_random(S + k + 1)  # fresh data: the tuned plan must compute it, not reuse
     enc.launch()
     torch.cuda.synchronize()
@@ -1208,7 +1212,8 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
 
 
 ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign",
-                   "realign-x8", "realign-x32"]
+                   "realign-x8", "realign-x32", "wix", "wix-g8", "wix-g2", "wix-q8", "wix-q16",
+                   "wix-x8", "wix-x32"]
 
 
 @pytest.mark.parametrize("k,m,S,batch,off,erase", [
@@ -1269,9 +1274,53 @@ def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, era
         assert {"x8", "x32"} <= set(taken), taken
         with pytest.raises(N.NativeError):
             plan.set_orders(["realign"])  # aligned shards: no realigning kernel
+    # 6-bit triple lookups: aligned shards, R <= 4 written rows, no Verify rows
+    rows = m if erase is None else len(erase)
+    wix_ok = (off % 16 == 0 and S % 16 == 0 and k >= 3 and rows <= 4
+              and (erase is None or n - len(erase) == k))
+    if wix_ok:
+        assert {"wix", "wix-g2", "wix-x32"} <= set(taken), taken
+    else:
+        assert not any(t.startswith("wix") for t in taken), taken
     with pytest.raises(N.NativeError):
         plan.set_orders(["none"] * (plan_groups := int(N.lib.rs_plan_groups(plan.handle))) + ["none"])
     plan.set_orders(["none"] * plan_groups)
+
+
+@pytest.mark.parametrize("k,m,S,order", [
+    (6, 4, 65_536 * 3 + 5, "wix"),        # two triples, no nibble shards
+    (4, 2, 1_000_003, "wix-g2"),           # one triple + 1
+    (5, 3, 262_147, "wix"),                # one triple + 2
+    (10, 4, 1 << 20, "wix"),               # the bench shape: 3 triples + 1
+    (12, 1, 100_000, "wix-x32"),           # R = 1
+    (16, 4, 262_144 + 48, "wix-x8"),
+    (20, 4, 1 << 18, "wix"),
+    (32, 4, 131_073, "wix-g2"),            # ragged tail through the nibble tables
+    (64, 2, 16_384 + 16, "wix"),
+    (128, 3, 8_192, "wix-x32"),            # 42 triples + 2
+])
+def test_plan_wix_triples_vs_oracle(native_lib, k, m, S, order):
+    """The 6-bit lookups over shard triples (Policy::WIX): every triple/remainder split
+    (K % 3 = 0, 1, 2), R = 1..4, ragged tails and several tile orders, every byte of
+    every stripe against the oracle's parity; constant stripes (all 0x00 / all 0xFF)
+    as the SURVEY's sanity inputs."""
+    import torch
+    from callfs_amd.device import Plan
+    n, batch = k + m, 3
+    pitch = (S + 255) // 256 * 256
+    buf = torch.randint(0, 256, (batch, n, pitch), dtype=torch.uint8, device="cuda:0")
+    buf[1, :k].fill_(0xFF)
+    buf[2, :k, : S // 2].zero_()
+    ptrs = [buf[b, i].data_ptr() for b in range(batch) for i in range(n)]
+    plan = Plan(k, m, S, batch, ptrs)
+    plan.set_orders([order])
+    plan.launch()
+    torch.cuda.synchronize()
+    h = buf.cpu().numpy()
+    for b in range(batch):
+        want = cref.encode([h[b, i, :S] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(h[b, k + j, :S], want[j]), (b, j)
 
 
 def test_plan_tune_argument_errors(native_lib):
@@ -1285,7 +1334,7 @@ def test_plan_tune_argument_errors(native_lib):
     assert N.lib.rs_plan_tune(None, None, 1, None, 0) == N.RS_E_ARG
     out = (ctypes.c_int * 3)(-7, -7, -7)
     assert N.lib.rs_plan_tune(p.handle, None, 1, out, 3) == 0
-    assert out[0] in range(7) and out[1] == -1 and out[2] == -1
+    assert (out[0] in range(7) or out[0] in range(64, 71)) and out[1] == -1 and out[2] == -1
 
 
 @pytest.mark.parametrize("k,m,S,batch,off", [(10, 4, 100_003, 3, 3), (4, 2, 65_537, 5, 1),
