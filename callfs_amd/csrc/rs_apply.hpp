@@ -108,7 +108,8 @@ template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS
 struct Policy {
   // LDS kernel, R <= 4, plain ring-of-three loop: input shards in triples, each byte
   // position of a triple resolved by four 6-bit lookups into 64-entry tables of 4-byte
-  // entries (built in LDS from the nibble tables) instead of six nibble lookups
+  // entries (built in LDS from the nibble tables) instead of six nibble lookups; Verify
+  // rows load their compared vectors after the input loop
   static constexpr bool WIX = WIX_;
   static_assert(!WIX_ || (REALIGN_ == 0 && RING_ == 0 && VPF_ == 0 && !NOMATH_ && !SDWA_),
                 "WIX: plain ring-of-three encode kernel only");

@@ -322,11 +322,11 @@ bool takes_lds(const ApplyArgs& a) { return a.R >= kLdsMinRows || a.K >= kLdsMin
 bool can_realign(const ApplyArgs& a) {
   return a.R <= 8 && (a.in_misalign || a.out_misalign) && realign_out_enabled();
 }
-// 6-bit triple lookups (Policy::WIX): R <= 4, K >= 3, aligned shards, no Verify rows
+// 6-bit triple lookups (Policy::WIX): R <= 4, K >= 3, aligned shards
 bool can_wix(const ApplyArgs& a) {
-  const uint32_t rows = (1u << a.R) - 1;
-  return a.R <= 4 && a.K >= 3 && !(a.in_misalign | a.out_misalign) && !(a.verify_mask & rows);
+  return a.R <= 4 && a.K >= 3 && !(a.in_misalign | a.out_misalign);
 }
+bool has_verify_rows(const ApplyArgs& a) { return (a.verify_mask & ((1u << a.R) - 1)) != 0; }
 // CALLFS_RS_WIX=0 keeps every launch on the nibble kernel (A/B)
 bool wix_enabled() {
   static const bool on = [] {
@@ -343,7 +343,10 @@ bool wix_enabled() {
 // RS(8,4) 76.5 -> 80.1 (128 KiB shards: equal); from K = 9 on equal or slower (RS(9,4) and
 // RS(10,4) equal, RS(12,3) -1.5, RS(16,4) -1.5, RS(20,4) -1.2, RS(32,4) -1.4), where
 // rs_plan_tune still times it for K <= 12.
-bool takes_wix(const ApplyArgs& a) { return can_wix(a) && a.K <= 8 && wix_enabled(); }
+// Launches with Verify rows keep the nibble kernel with its early compare loads (VPF).
+bool takes_wix(const ApplyArgs& a) {
+  return can_wix(a) && a.K <= 8 && !has_verify_rows(a) && wix_enabled();
+}
 bool takes_realign(const ApplyArgs& a) {
   return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u);
 }
@@ -405,7 +408,7 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(TileOrder::kXcd8);
       add(TileOrder::kXcd32);
     }
-    if (can_wix(a) && (every_instance || (a.K <= 12 && wix_enabled()))) {
+    if (can_wix(a) && (every_instance || (a.K <= 12 && !has_verify_rows(a) && wix_enabled()))) {
       // timed up to K = 12 (equal at 9..10 on one box, -1.5 at 12); every instance on request
       const int n0 = static_cast<int>(c.size());
       for (int i = 0; i < n0; ++i)

@@ -1220,6 +1220,7 @@ ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign
     (10, 4, (1 << 20) + 16, 3, 0, None),   # aligned: 129 tiles per stripe, X8/X32 groups + tail
     (10, 4, (1 << 20) + 1, 3, 1, None),    # Split layout (odd S): realigning kernel per order
     (10, 4, (1 << 20) + 1, 3, 1, (5,)),    # one erasure: 1 written + 3 Verify rows
+    (6, 3, (1 << 18) + 32, 3, 0, (2,)),    # aligned, 1 written + 2 Verify rows (WIX too)
     (10, 8, 300_001, 5, 3, None),          # R = 8, realigning kernel
     (4, 2, 8 * 512 * 16 * 9 + 7, 2, 0, (0, 1)),  # k = 4, R = 2 decode, ragged tail
 ])
@@ -1274,10 +1275,9 @@ def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, era
         assert {"x8", "x32"} <= set(taken), taken
         with pytest.raises(N.NativeError):
             plan.set_orders(["realign"])  # aligned shards: no realigning kernel
-    # 6-bit triple lookups: aligned shards, R <= 4 written rows, no Verify rows
-    rows = m if erase is None else len(erase)
-    wix_ok = (off % 16 == 0 and S % 16 == 0 and k >= 3 and rows <= 4
-              and (erase is None or n - len(erase) == k))
+    # 6-bit triple lookups: aligned shards, one launch group of R = m <= 4 rows (written
+    # or compared), K >= 4 (the LDS kernel)
+    wix_ok = off % 16 == 0 and S % 16 == 0 and k >= 4 and m <= 4
     if wix_ok:
         assert {"wix", "wix-g2", "wix-x32"} <= set(taken), taken
     else:
