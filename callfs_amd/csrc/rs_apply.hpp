@@ -104,13 +104,14 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //            global_load_dwordx4
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
           int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, int REALIGN_ = 0,
-          bool SDWA_ = false, int PROBE_ = 0, int VPF_ = 0, bool WIX_ = false>
+          bool SDWA_ = false, int PROBE_ = 0, int VPF_ = 0, int WIX_ = 0>
 struct Policy {
   // LDS kernel, R <= 4, plain ring-of-three loop: input shards in triples, each byte
   // position of a triple resolved by four 6-bit lookups into 64-entry tables of 4-byte
   // entries (built in LDS from the nibble tables) instead of six nibble lookups; Verify
   // rows load their compared vectors after the input loop
-  static constexpr bool WIX = WIX_;
+  // (WIX 2, A/B probe: the same triple loop with the nibble lookups, any R <= 8)
+  static constexpr int WIX = WIX_;
   static_assert(!WIX_ || (REALIGN_ == 0 && RING_ == 0 && VPF_ == 0 && !NOMATH_ && !SDWA_),
                 "WIX: plain ring-of-three encode kernel only");
   // > 0: Verify rows' stored vectors are loaded VPF shards before the end of the input
@@ -724,7 +725,7 @@ void rs_apply_lds(ApplyArgs a) {
     for (int j = threadIdx.x; j < K * 2 * W; j += BS) dst[j] = src[j];
   }
   __syncthreads();
-  if constexpr (P::WIX) {  // the triples' 6-bit tables, from the nibble tables
+  if constexpr (P::WIX == 1) {  // the triples' 6-bit tables, from the nibble tables
     const uint32_t l0 = static_cast<uint32_t>(
         reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)smem));
     const uint32_t n = static_cast<uint32_t>(K / 3) * 256u;
@@ -799,7 +800,14 @@ void rs_apply_lds(ApplyArgs a) {
         const int i = 3 * g + 3;
         const uint4 n0 = i < K ? ld(i) : x0, n1 = i + 1 < K ? ld(i + 1) : x0,
                     n2 = i + 2 < K ? ld(i + 2) : x0;
-        wix_mac<RT>(acc, x0, x1, x2, lds0 + wix_base(K) + 1024u * static_cast<uint32_t>(g));
+        if constexpr (P::WIX == 1) {
+          wix_mac<RT>(acc, x0, x1, x2, lds0 + wix_base(K) + 1024u * static_cast<uint32_t>(g));
+        } else {
+          const uint32_t b = lds0 + static_cast<uint32_t>(3 * g) * 32u * W;
+          lds_mac<RT>(acc, x0, b);
+          lds_mac<RT>(acc, x1, b + 32u * W);
+          lds_mac<RT>(acc, x2, b + 64u * W);
+        }
         x0 = n0;
         x1 = n1;
         x2 = n2;

@@ -86,7 +86,11 @@ using LdsVerifyPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, fal
 // R <= 4 with 6-bit lookups over shard triples (rs_apply.hpp Policy::WIX): 4 lookups per
 // byte position of three shards instead of 6; one instance per tile order.
 template <int ORD>
-using LdsWixPolicy = dev::Policy<8, 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, true>;
+using LdsWixPolicy = dev::Policy<8, 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, 1>;
+// A/B probe (orders kOrderTri + TileOrder, rs_plan_set_orders only): the same triple loop
+// with nibble lookups, R <= 8
+template <int R, int ORD>
+using LdsTriPolicy = dev::Policy<(R <= 4 ? 8 : 2), 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, 2>;
 template <int ORD>
 using LdsRealignOutPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 2>;
 template <int ORD>
@@ -230,6 +234,15 @@ const std::array<std::array<VecFn, 4>, kTileOrders> kLdsWix = {
     lds_order_table<LdsWixPolicy<8>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsWixPolicy<10>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsWixPolicy<11>>(std::make_integer_sequence<int, 4>{})};
+template <int ORD, int... Rs>
+constexpr auto lds_tri_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsTriPolicy<Rs + 1, ORD>>...};
+}
+// [consecutive, G2, X32][R - 1]
+const std::array<std::array<VecFn, 8>, 3> kLdsTri = {
+    lds_tri_table<0>(std::make_integer_sequence<int, 8>{}),
+    lds_tri_table<5>(std::make_integer_sequence<int, 8>{}),
+    lds_tri_table<11>(std::make_integer_sequence<int, 8>{})};
 template <int ORD, int... Rs>
 constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1, ORD>>...};
@@ -408,6 +421,11 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(TileOrder::kXcd8);
       add(TileOrder::kXcd32);
     }
+    if (every_instance && a.K >= 3 && !(a.in_misalign | a.out_misalign)) {
+      c.push_back(kOrderTri + static_cast<int>(TileOrder::kConsecutive));
+      c.push_back(kOrderTri + static_cast<int>(TileOrder::kGroup2));
+      c.push_back(kOrderTri + static_cast<int>(TileOrder::kXcd32));
+    }
     if (can_wix(a) && (every_instance || (a.K <= 12 && !has_verify_rows(a) && wix_enabled()))) {
       // timed up to K = 12 (equal at 9..10 on one box, -1.5 at 12); every instance on request
       const int n0 = static_cast<int>(c.size());
@@ -428,6 +446,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
+  const bool tri = order >= kOrderTri && a.R <= 8 && a.K >= 3;
+  if (order >= kOrderTri) order = tri ? order - kOrderTri : -1;
   const bool wix = order >= kOrderWix ? can_wix(a) : order < 0 && takes_wix(a);
   if (order >= kOrderWix) order -= kOrderWix;
   uint64_t tail0 = 0;
@@ -464,6 +484,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
             fn = kLdsWix[oi][a.R - 1];
             lds = dev::lds_bytes_wix(a.K);
           }
+          if (tri)
+            fn = kLdsTri[ord == TileOrder::kGroup2 ? 1 : ord == TileOrder::kXcd32 ? 2 : 0][a.R - 1];
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }
@@ -584,6 +606,7 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
   a.tail_in_vec = a.nvec * 16 < a.S;
+  if (order >= kOrderTri) order -= kOrderTri;
   if (order >= kOrderWix) order -= kOrderWix;  // bounded by the nibble kernel's traffic
   // the order the production launch would take (a tuned order, else the rule; the
   // realigning and v_perm launches are bounded by the plain kernel's traffic)

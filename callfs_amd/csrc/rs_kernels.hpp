@@ -108,6 +108,8 @@ constexpr int kOrderRealign = 32;
 // (kOrderWix + a TileOrder: the R <= 4 LDS kernel with 6-bit lookups over shard triples,
 // rs_apply.hpp Policy::WIX; aligned launches without Verify rows, K >= 3)
 constexpr int kOrderWix = 64;
+// (kOrderTri + consecutive / G2 / X32: A/B probe, the triple loop with nibble lookups)
+constexpr int kOrderTri = 96;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the

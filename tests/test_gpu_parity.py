@@ -1213,7 +1213,7 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
 
 ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign",
                    "realign-x8", "realign-x32", "wix", "wix-g8", "wix-g2", "wix-q8", "wix-q16",
-                   "wix-x8", "wix-x32"]
+                   "wix-x8", "wix-x32", "tri", "tri-g2", "tri-x32"]
 
 
 @pytest.mark.parametrize("k,m,S,batch,off,erase", [

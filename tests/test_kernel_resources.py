@@ -41,8 +41,10 @@ def _policy(k):
 
 def _lds(ks):
     """Production LDS-kernel instances (the NOMATH ceiling forms, Policy argument 10, are
-    measurement kernels of rs_plan_launch_ceiling and excluded)."""
-    return [k for k in ks if "rs_apply_lds<" in k["name"] and _policy(k)[9] != "true"]
+    measurement kernels of rs_plan_launch_ceiling, and WIX 2, argument 15, an A/B probe
+    reachable only through rs_plan_set_orders: both excluded)."""
+    return [k for k in ks if "rs_apply_lds<" in k["name"] and _policy(k)[9] != "true"
+            and _policy(k)[14] != "2"]
 
 
 def test_every_kernel_reported(kernels):
