@@ -358,7 +358,8 @@ bool wix_enabled() {
 // rs_plan_tune still times it for K <= 12.
 // Launches with Verify rows keep the nibble kernel with its early compare loads (VPF).
 bool takes_wix(const ApplyArgs& a) {
-  return can_wix(a) && a.K <= 8 && !has_verify_rows(a) && wix_enabled();
+  return wix_enabled() && takes_lds(a) &&
+         wix_rule(a.K, a.R, (a.in_misalign | a.out_misalign) != 0, has_verify_rows(a));
 }
 bool takes_realign(const ApplyArgs& a) {
   return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u);
@@ -426,7 +427,8 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       c.push_back(kOrderTri + static_cast<int>(TileOrder::kGroup2));
       c.push_back(kOrderTri + static_cast<int>(TileOrder::kXcd32));
     }
-    if (can_wix(a) && (every_instance || (a.K <= 12 && !has_verify_rows(a) && wix_enabled()))) {
+    if (can_wix(a) && (every_instance ||
+                       (wix_enabled() && wix_tunable(a.K, a.R, false, has_verify_rows(a))))) {
       // timed up to K = 12 (equal at 9..10 on one box, -1.5 at 12); every instance on request
       const int n0 = static_cast<int>(c.size());
       for (int i = 0; i < n0; ++i)

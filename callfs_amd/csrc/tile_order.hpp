@@ -129,6 +129,17 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
   return TileOrder::kConsecutive;
 }
 
+// Kernel form of an aligned R <= 4 LDS launch (rs_kernels.hip takes_wix, DESIGN.md §5
+// "Six-bit lookups over shard triples"): the 6-bit triple lookups where they measured
+// 1.4-7.5 points faster, 4 <= K <= 8 without Verify rows (the nibble kernel keeps its
+// early compare loads); misaligned shards take the realigning kernel instead.
+inline bool wix_rule(int K, int R, bool misaligned, bool verify) {
+  return R <= 4 && K >= 4 && K <= 8 && !misaligned && !verify;
+}
+// rs_plan_tune also times the WIX instances up to K = 12 (a wash at 9..10, -1.5 at 12)
+inline bool wix_tunable(int K, int R, bool misaligned, bool verify) {
+  return R <= 4 && K >= 3 && K <= 12 && !misaligned && !verify;
+}
 // Wide groups hold 19-32 shard streams per stripe; from 2 MiB shards on, 8 interleaved
 // column segments beat consecutive tiles (tools/order_sweep.sh, KB_ORD, 9 rounds, % of
 // 8 TB/s: RS(10,12) 4 MiB 60.3 -> 66.9, RS(10,16) 16 MiB 58.0 -> 66.7; at 1 MiB all
