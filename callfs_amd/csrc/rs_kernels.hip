@@ -335,9 +335,10 @@ bool takes_lds(const ApplyArgs& a) { return a.R >= kLdsMinRows || a.K >= kLdsMin
 bool can_realign(const ApplyArgs& a) {
   return a.R <= 8 && (a.in_misalign || a.out_misalign) && realign_out_enabled();
 }
-// 6-bit triple lookups (Policy::WIX): R <= 4, K >= 3, aligned shards
+// 6-bit triple lookups (Policy::WIX): R <= 4, 3 <= K <= 96 (tables within the 64 KiB of
+// dynamic LDS a launch gets without the opt-in), aligned shards
 bool can_wix(const ApplyArgs& a) {
-  return a.R <= 4 && a.K >= 3 && !(a.in_misalign | a.out_misalign);
+  return a.R <= 4 && a.K >= 3 && a.K <= 96 && !(a.in_misalign | a.out_misalign);
 }
 bool has_verify_rows(const ApplyArgs& a) { return (a.verify_mask & ((1u << a.R) - 1)) != 0; }
 // CALLFS_RS_WIX=0 keeps every launch on the nibble kernel (A/B)
@@ -482,7 +483,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           const int oi = static_cast<int>(ord);
           if (a.R <= 4 && (a.verify_mask & rows) && oi >= 0 && oi < kTileOrders)
             fn = kLdsVerify[oi][a.R - 1];
-          if (wix && oi >= 0 && oi < kTileOrders) {  // (at most 42 KiB of tables at K = 128)
+          if (wix && oi >= 0 && oi < kTileOrders) {  // (at most 56 KiB of tables at K = 96)
             fn = kLdsWix[oi][a.R - 1];
             lds = dev::lds_bytes_wix(a.K);
           }

@@ -1297,7 +1297,7 @@ def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, era
     (20, 4, 1 << 18, "wix"),
     (32, 4, 131_073, "wix-g2"),            # ragged tail through the nibble tables
     (64, 2, 16_384 + 16, "wix"),
-    (128, 3, 8_192, "wix-x32"),            # 42 triples + 2
+    (96, 3, 8_192, "wix-x32"),             # 32 triples: the largest K offered (56 KiB LDS)
 ])
 def test_plan_wix_triples_vs_oracle(native_lib, k, m, S, order):
     """The 6-bit lookups over shard triples (Policy::WIX): every triple/remainder split
