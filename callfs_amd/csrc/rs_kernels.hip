@@ -341,7 +341,7 @@ bool can_wix(const ApplyArgs& a) {
   return a.R <= 4 && a.K >= 3 && a.K <= 96 && !(a.in_misalign | a.out_misalign);
 }
 bool has_verify_rows(const ApplyArgs& a) { return (a.verify_mask & ((1u << a.R) - 1)) != 0; }
-// CALLFS_RS_WIX=0 keeps every launch on the nibble kernel (A/B)
+// CALLFS_RS_WIX=0 keeps every launch on the ring-of-three nibble kernel (A/B)
 bool wix_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("CALLFS_RS_WIX");
@@ -349,19 +349,30 @@ bool wix_enabled() {
   }();
   return on;
 }
-// The rule takes it for 4 <= K <= 8 (K = 3 runs the v_perm kernel), in the nibble rule's
-// tile order. tools/wix_ab*.sh, profiles/r03/wix/, % of 8 TB/s, best nibble order -> WIX
-// in the rule's order, one box: RS(4,2) 1 MiB 72.3 -> 79.0-79.6 (4 MiB 71.4 -> 78.6, 1 MiB
-// objects 71.4 -> 77.4), RS(4,4) 75.0 -> 81.5, RS(5,2) 73.3 -> 78.9, RS(5,3) 74.5 -> 79.9,
-// RS(6,2) 74.6 -> 77.5, RS(6,3) 74.1 -> 75.5, RS(7,3) 75.1 -> 77.3, RS(8,2) 74.9 -> 77.7,
-// RS(8,4) 76.5 -> 80.1 (128 KiB shards: equal); from K = 9 on equal or slower (RS(9,4) and
-// RS(10,4) equal, RS(12,3) -1.5, RS(16,4) -1.5, RS(20,4) -1.2, RS(32,4) -1.4), where
-// rs_plan_tune still times it for K <= 12.
-// Launches with Verify rows keep the nibble kernel with its early compare loads (VPF).
-bool takes_wix(const ApplyArgs& a) {
+// Since the triple-load form (below) measured equal or faster than WIX everywhere, the
+// rule no longer takes WIX: its instances remain for rs_plan_set_orders (A/B).
+// tools/wix_ab*.sh, profiles/r03/wix/: WIX in the nibble rule's order vs the nibble kernel's
+// best order, 1 MiB shards: RS(4,2) 72.3 -> 79.0, RS(4,4) 75.0 -> 81.5, RS(5,3) 74.5 -> 79.9,
+// RS(8,4) 76.5 -> 80.1; RS(10,4) equal, RS(16,4) / RS(20,4) / RS(32,4) -1.2 ... -1.5.
+
+// Triple loads (Policy::WIX 2): tile_order.hpp tri_rule. tools/wix_ab4.sh,
+// profiles/r03/wix/ab4_tri_verify.jsonl, % of 8 TB/s, nibble (best order) -> triples in
+// the rule's order: RS(4,2) 71.8 -> 80.6, RS(5,3) 74.6 -> 80.3, RS(8,4) 76.3 -> 80.2,
+// RS(10,4) 75.8 -> 76.6, RS(6,6) 74.6 -> 75.7, RS(8,8) 75.4 -> 76.3, RS(10,8) 74.1 -> 77.4;
+// read-only (download Verify): RS(4,2) 82.5 -> 88.4, RS(10,4) 83.8 -> 86.0 (X32).
+bool takes_tri(const ApplyArgs& a) {
+  const uint32_t rows = (1u << a.R) - 1;
+  const uint64_t tps = (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;
   return wix_enabled() && takes_lds(a) &&
-         wix_rule(a.K, a.R, (a.in_misalign | a.out_misalign) != 0, has_verify_rows(a));
+         tri_rule(a.K, a.R, (a.in_misalign | a.out_misalign) != 0, (a.verify_mask & rows) != 0,
+                  (a.verify_mask & rows) == rows, tps);
 }
+bool tri_tunable_launch(const ApplyArgs& a) {
+  const uint32_t rows = (1u << a.R) - 1;
+  return wix_enabled() && tri_tunable(a.K, a.R, (a.in_misalign | a.out_misalign) != 0,
+                                      (a.verify_mask & rows) != 0, (a.verify_mask & rows) == rows);
+}
+int tri_index(TileOrder o) { return o == TileOrder::kGroup2 ? 1 : o == TileOrder::kXcd32 ? 2 : 0; }
 bool takes_realign(const ApplyArgs& a) {
   return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u);
 }
@@ -404,7 +415,10 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       return static_cast<TileOrder>(kOrderWix + static_cast<int>(o));
     };
     if (takes_realign(a)) add(realign_in(TileOrder::kXcd32));
-    if (takes_wix(a)) add(wix_in(lds_rule(a)));  // the rule's kernel first
+    const auto tri_in = [](TileOrder o) {
+      return static_cast<TileOrder>(kOrderTri + static_cast<int>(o));
+    };
+    if (takes_tri(a)) add(tri_in(tri_order(lds_rule(a))));  // the rule's kernel first
     add(lds_rule(a));
     if (can_realign(a)) {
       add(realign_in(TileOrder::kXcd32));
@@ -423,14 +437,12 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(TileOrder::kXcd8);
       add(TileOrder::kXcd32);
     }
-    if (every_instance && a.K >= 3 && !(a.in_misalign | a.out_misalign)) {
-      c.push_back(kOrderTri + static_cast<int>(TileOrder::kConsecutive));
-      c.push_back(kOrderTri + static_cast<int>(TileOrder::kGroup2));
-      c.push_back(kOrderTri + static_cast<int>(TileOrder::kXcd32));
+    if ((every_instance && a.K >= 3 && !(a.in_misalign | a.out_misalign)) || tri_tunable_launch(a)) {
+      add(tri_in(TileOrder::kConsecutive));
+      add(tri_in(TileOrder::kGroup2));
+      add(tri_in(TileOrder::kXcd32));
     }
-    if (can_wix(a) && (every_instance ||
-                       (wix_enabled() && wix_tunable(a.K, a.R, false, has_verify_rows(a))))) {
-      // timed up to K = 12 (equal at 9..10 on one box, -1.5 at 12); every instance on request
+    if (every_instance && can_wix(a)) {  // WIX: A/B instances only
       const int n0 = static_cast<int>(c.size());
       for (int i = 0; i < n0; ++i)
         if (c[i] >= 0 && c[i] < kTileOrders) add(wix_in(static_cast<TileOrder>(c[i])));
@@ -449,9 +461,9 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
-  const bool tri = order >= kOrderTri && a.R <= 8 && a.K >= 3;
+  bool tri = order >= kOrderTri && a.R <= 8 && a.K >= 3;
   if (order >= kOrderTri) order = tri ? order - kOrderTri : -1;
-  const bool wix = order >= kOrderWix ? can_wix(a) : order < 0 && takes_wix(a);
+  const bool wix = order >= kOrderWix && can_wix(a);
   if (order >= kOrderWix) order -= kOrderWix;
   uint64_t tail0 = 0;
   a.tail_in_vec = 0;
@@ -487,8 +499,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
             fn = kLdsWix[oi][a.R - 1];
             lds = dev::lds_bytes_wix(a.K);
           }
-          if (tri)
-            fn = kLdsTri[ord == TileOrder::kGroup2 ? 1 : ord == TileOrder::kXcd32 ? 2 : 0][a.R - 1];
+          if (!tri && order < 0 && takes_tri(a)) tri = true;  // the rule: ord is the nibble rule's
+          if (tri) fn = kLdsTri[tri_index(order < 0 ? tri_order(ord) : ord)][a.R - 1];
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }

@@ -129,16 +129,29 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
   return TileOrder::kConsecutive;
 }
 
-// Kernel form of an aligned R <= 4 LDS launch (rs_kernels.hip takes_wix, DESIGN.md §5
-// "Six-bit lookups over shard triples"): the 6-bit triple lookups where they measured
-// 1.4-7.5 points faster, 4 <= K <= 8 without Verify rows (the nibble kernel keeps its
-// early compare loads); misaligned shards take the realigning kernel instead.
-inline bool wix_rule(int K, int R, bool misaligned, bool verify) {
-  return R <= 4 && K >= 4 && K <= 8 && !misaligned && !verify;
+// Triple-load form of an aligned R <= 8 LDS launch (Policy::WIX 2, rs_kernels.hip
+// takes_tri; DESIGN.md §5 "Shard triples"): the loads of three input shards issued
+// together, then their nibble lookups. Taken for 4 <= K <= 10 up to 8 MiB shards (tps <=
+// 1024) by launches that write every row or compare every row; launches that mix written
+// and Verify rows keep the ring of three with its early compare loads (one-erasure decodes
+// ran 0.3-1.5 points slower in triples).
+inline bool tri_rule(int K, int R, bool misaligned, bool verify, bool read_only, uint64_t tps) {
+  return R <= 8 && K >= 4 && K <= 10 && !misaligned && (!verify || read_only) && tps <= 1024;
 }
-// rs_plan_tune also times the WIX instances up to K = 12 (a wash at 9..10, -1.5 at 12)
-inline bool wix_tunable(int K, int R, bool misaligned, bool verify) {
-  return R <= 4 && K >= 3 && K <= 12 && !misaligned && !verify;
+// rs_plan_tune also times the triple form up to K = 12
+inline bool tri_tunable(int K, int R, bool misaligned, bool verify, bool read_only) {
+  return R <= 8 && K >= 3 && K <= 12 && !misaligned && (!verify || read_only);
+}
+// The triple form's tile order (instances: consecutive, G2, X32) for the order the nibble
+// rule picks: G8 (shards up to 256 KiB) -> X32, which ran within 0.6 points of G8 for the
+// 6-bit form at 1 MiB objects.
+inline TileOrder tri_order(TileOrder nibble) {
+  switch (nibble) {
+    case TileOrder::kGroup2: return TileOrder::kGroup2;
+    case TileOrder::kGroup8:
+    case TileOrder::kXcd32: return TileOrder::kXcd32;
+    default: return TileOrder::kConsecutive;
+  }
 }
 // Wide groups hold 19-32 shard streams per stripe; from 2 MiB shards on, 8 interleaved
 // column segments beat consecutive tiles (tools/order_sweep.sh, KB_ORD, 9 rounds, % of

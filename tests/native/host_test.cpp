@@ -287,16 +287,23 @@ int main() {
     CHECK(vec_tile_order(349526, tps_of(349526), 8) == TileOrder::kGroup2);
     CHECK(vec_tile_order(16 * MiB, tps_of(16 * MiB), 24) == TileOrder::kSeg16);
     CHECK(vec_tile_order(107374183, tps_of(107374183), 8) == TileOrder::kConsecutive);
-    // 6-bit triple lookups: aligned R <= 4 launches with 4..8 inputs and no Verify rows
-    CHECK(wix_rule(4, 2, false, false));   // CallFS default RS(4,2) encode
-    CHECK(wix_rule(8, 4, false, false));
-    CHECK(!wix_rule(3, 2, false, false));  // k = 3: the v_perm kernel
-    CHECK(!wix_rule(10, 4, false, false)); // the bench shape: the tuner decides
-    CHECK(!wix_rule(4, 2, true, false));   // Split layout: realigning kernel
-    CHECK(!wix_rule(6, 3, false, true));   // Verify rows keep the early compare loads
-    CHECK(!wix_rule(8, 5, false, false));  // 8-byte entries
-    CHECK(wix_tunable(10, 4, false, false) && wix_tunable(12, 1, false, false));
-    CHECK(!wix_tunable(16, 4, false, false) && !wix_tunable(10, 4, false, true));
+    // triple loads: aligned R <= 8 launches with 4..10 inputs that write every row or
+    // compare every row, shards up to 8 MiB
+    const uint64_t t1 = tps_of(MiB);
+    CHECK(tri_rule(4, 2, false, false, false, t1));   // CallFS default RS(4,2) encode
+    CHECK(tri_rule(10, 4, false, false, false, t1));  // the bench shape
+    CHECK(tri_rule(8, 8, false, false, false, t1));   // 8-byte entries too
+    CHECK(tri_rule(4, 2, false, true, true, t1));     // download Verify (read-only)
+    CHECK(!tri_rule(3, 2, false, false, false, t1));  // k = 3: the v_perm kernel
+    CHECK(!tri_rule(12, 4, false, false, false, t1)); // the tuner decides
+    CHECK(!tri_rule(4, 2, true, false, false, t1));   // Split layout: realigning kernel
+    CHECK(!tri_rule(6, 3, false, true, false, t1));   // written + Verify rows: early compares
+    CHECK(!tri_rule(10, 9, false, false, false, t1)); // 16-byte entries
+    CHECK(!tri_rule(4, 2, false, false, false, tps_of(16 * MiB)));
+    CHECK(tri_tunable(12, 4, false, false, false) && !tri_tunable(16, 4, false, false, false));
+    CHECK(tri_order(TileOrder::kGroup8) == TileOrder::kXcd32);
+    CHECK(tri_order(TileOrder::kGroup2) == TileOrder::kGroup2);
+    CHECK(tri_order(TileOrder::kConsecutive) == TileOrder::kConsecutive);
   }
   // 6. multi-device placement (dispatch.hpp), mocked device counts
   {

@@ -1180,9 +1180,9 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
     names = enc.tune(reps=1)
     assert len(names) == max(1, -(-m // 16))
     plain = {"consecutive", "g8", "g2", "q8", "q16", "x8", "x32"}
-    # an encode plan with R <= 4 rows may also take the 6-bit triple lookups (K <= 12)
-    wix_ok = 4 <= k <= 12 and m <= 4
-    allowed = plain | ({"wix-" + o for o in plain} | {"wix"} if wix_ok else set())
+    # an encode plan with R <= 8 rows and 3..12 inputs may also take the triple loads
+    tri_ok = 3 <= k <= 12 and m <= 8
+    allowed = plain | ({"tri", "tri-g2", "tri-x32"} if tri_ok else set())
     assert all(n in allowed for n in names), names
     sb.fill_random(S + k + 1)  # fresh data: the tuned plan must compute it, not reuse
     enc.launch()
@@ -1323,6 +1323,50 @@ def test_plan_wix_triples_vs_oracle(native_lib, k, m, S, order):
             assert np.array_equal(h[b, k + j, :S], want[j]), (b, j)
 
 
+@pytest.mark.parametrize("k,m,S,erase", [
+    (4, 2, (1 << 20) + 16, None),        # CallFS default profile, encode: rule = triples
+    (8, 8, 262_144 + 5, None),           # R = 8 (8-byte entries), ragged tail
+    (6, 6, 65_536, None),                # 1 MiB-object-sized shards (G8 -> X32)
+    (10, 8, 300_000, None),
+    (10, 4, 1 << 20, (0, 1, 2, 3)),      # the bench decode
+    (4, 2, 1 << 20, ()),                 # download Verify, nothing erased: read-only
+    (10, 4, 100_000 + 3, ()),            # read-only, ragged tail compared too
+    (5, 3, 1 << 18, (1,)),               # written + Verify rows: ring of three (no triples)
+])
+def test_plan_rule_triples_vs_oracle(native_lib, k, m, S, erase):
+    """The rule's triple-load kernel (4 <= K <= 10, R <= 8, launches that write every row
+    or compare every row): encode / reconstruct every byte of every stripe as the oracle
+    does; read-only launches pass clean stripes and flag exactly the stripe with a flipped
+    byte, also in the ragged tail."""
+    import torch
+    from callfs_amd.device import Plan
+    n, batch = k + m, 3
+    pitch = (S + 255) // 256 * 256
+    buf = torch.randint(0, 256, (batch, n, pitch), dtype=torch.uint8, device="cuda:0")
+    ptrs = [buf[b, i].data_ptr() for b in range(batch) for i in range(n)]
+    Plan(k, m, S, batch, ptrs).launch()
+    torch.cuda.synchronize()
+    h = buf.cpu().numpy()
+    for b in range(batch):
+        want = cref.encode([h[b, i, :S] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(h[b, k + j, :S], want[j]), (b, j)
+    if erase is None:
+        return
+    good = buf.clone()
+    dec = Plan(k, m, S, batch, ptrs, present=[i not in erase for i in range(n)])
+    for i in erase:
+        buf[:, i].zero_()
+    dec.launch()
+    assert not dec.corrupt()
+    assert torch.equal(buf[:, :, :S], good[:, :, :S])
+    if len(erase) < m:  # a Verify row exists
+        row = n - 1
+        buf[2, row, S - 1] ^= 0x01  # last byte: the ragged tail when S % 16 != 0
+        dec.launch()
+        assert dec.corrupt_stripes() == [2]
+
+
 def test_plan_tune_argument_errors(native_lib):
     import ctypes
     from callfs_amd import _native as N
@@ -1334,7 +1378,7 @@ def test_plan_tune_argument_errors(native_lib):
     assert N.lib.rs_plan_tune(None, None, 1, None, 0) == N.RS_E_ARG
     out = (ctypes.c_int * 3)(-7, -7, -7)
     assert N.lib.rs_plan_tune(p.handle, None, 1, out, 3) == 0
-    assert (out[0] in range(7) or out[0] in range(64, 71)) and out[1] == -1 and out[2] == -1
+    assert out[0] in (*range(7), 96, 98, 102) and out[1] == -1 and out[2] == -1
 
 
 @pytest.mark.parametrize("k,m,S,batch,off", [(10, 4, 100_003, 3, 3), (4, 2, 65_537, 5, 1),

@@ -41,10 +41,8 @@ def _policy(k):
 
 def _lds(ks):
     """Production LDS-kernel instances (the NOMATH ceiling forms, Policy argument 10, are
-    measurement kernels of rs_plan_launch_ceiling, and WIX 2, argument 15, an A/B probe
-    reachable only through rs_plan_set_orders: both excluded)."""
-    return [k for k in ks if "rs_apply_lds<" in k["name"] and _policy(k)[9] != "true"
-            and _policy(k)[14] != "2"]
+    measurement kernels of rs_plan_launch_ceiling and excluded)."""
+    return [k for k in ks if "rs_apply_lds<" in k["name"] and _policy(k)[9] != "true"]
 
 
 def test_every_kernel_reported(kernels):
@@ -65,12 +63,14 @@ def test_no_scratch_or_spills(kernels):
 
 
 def test_lds_kernel_occupancy(kernels):
-    """R <= 4: 8 waves; R 5..8: at least 7 (6 for the realigning form); R 9..16
+    """R <= 4: 8 waves; R 5..8: at least 7 (6 for the realigning form, 5 for the triple
+    loads); R 9..16
     (16-byte entries): 4 waves."""
     for k in _lds(kernels):
         r = int(re.search(r"rs_apply_lds<(\d+),", k["name"]).group(1))
         realign = _policy(k)[10] not in ("false", "0")
-        want = 8 if r <= 4 else (6 if realign else 7) if r <= 8 else 4
+        triple = _policy(k)[14] == "2"  # triple loads: 12 more VGPRs, measured at 5 waves
+        want = 8 if r <= 4 else (6 if realign else 5 if triple else 7) if r <= 8 else 4
         assert k["waves_per_simd"] >= want, (k["name"], k["vgprs"], k["waves_per_simd"])
         if r > 8:
             assert k["vgprs"] + k.get("agprs", 0) <= 128, k["name"]
