@@ -359,7 +359,11 @@ bool wix_enabled() {
 // profiles/r03/wix/ab4_tri_verify.jsonl, % of 8 TB/s, nibble (best order) -> triples in
 // the rule's order: RS(4,2) 71.8 -> 80.6, RS(5,3) 74.6 -> 80.3, RS(8,4) 76.3 -> 80.2,
 // RS(10,4) 75.8 -> 76.6, RS(6,6) 74.6 -> 75.7, RS(8,8) 75.4 -> 76.3, RS(10,8) 74.1 -> 77.4;
-// read-only (download Verify): RS(4,2) 82.5 -> 88.4, RS(10,4) 83.8 -> 86.0 (X32).
+// read-only (download Verify): RS(4,2) 82.5 -> 88.4, RS(10,4) 83.8 -> 86.0 (X32). Second
+// box (profiles/r03/tri1/ab.jsonl), the rule itself: RS(4,2) 72.5 -> 80.6, 1 MiB objects
+// 71.9 -> 77.9, RS(8,8) 75.6 -> 77.6, RS(10,8) 74.4 -> 78.2, RS(4,2) read-only 82.8 ->
+// 88.0, RS(6,3) 1 MiB objects 71.4 -> 73.2, RS(10,4) 76.5 -> 75.9-76.1 (the tuner keeps
+// whichever is faster), RS(12,4) 77.2 -> 80.3 (G2).
 bool takes_tri(const ApplyArgs& a) {
   const uint32_t rows = (1u << a.R) - 1;
   const uint64_t tps = (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;

@@ -131,16 +131,17 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
 
 // Triple-load form of an aligned R <= 8 LDS launch (Policy::WIX 2, rs_kernels.hip
 // takes_tri; DESIGN.md §5 "Shard triples"): the loads of three input shards issued
-// together, then their nibble lookups. Taken for 4 <= K <= 10 up to 8 MiB shards (tps <=
+// together, then their nibble lookups. Taken for 4 <= K <= 12 up to 8 MiB shards (tps <=
 // 1024) by launches that write every row or compare every row; launches that mix written
 // and Verify rows keep the ring of three with its early compare loads (one-erasure decodes
-// ran 0.3-1.5 points slower in triples).
+// ran 0.3-1.5 points slower in triples). RS(12,4) 77.2 -> 80.3 in G2; RS(16,4) gained 0.7
+// there and is left to rs_plan_tune.
 inline bool tri_rule(int K, int R, bool misaligned, bool verify, bool read_only, uint64_t tps) {
-  return R <= 8 && K >= 4 && K <= 10 && !misaligned && (!verify || read_only) && tps <= 1024;
+  return R <= 8 && K >= 4 && K <= 12 && !misaligned && (!verify || read_only) && tps <= 1024;
 }
-// rs_plan_tune also times the triple form up to K = 12
+// rs_plan_tune also times the triple form up to K = 16
 inline bool tri_tunable(int K, int R, bool misaligned, bool verify, bool read_only) {
-  return R <= 8 && K >= 3 && K <= 12 && !misaligned && (!verify || read_only);
+  return R <= 8 && K >= 3 && K <= 16 && !misaligned && (!verify || read_only);
 }
 // The triple form's tile order (instances: consecutive, G2, X32) for the order the nibble
 // rule picks: G8 (shards up to 256 KiB) -> X32, which ran within 0.6 points of G8 for the

@@ -295,12 +295,13 @@ int main() {
     CHECK(tri_rule(8, 8, false, false, false, t1));   // 8-byte entries too
     CHECK(tri_rule(4, 2, false, true, true, t1));     // download Verify (read-only)
     CHECK(!tri_rule(3, 2, false, false, false, t1));  // k = 3: the v_perm kernel
-    CHECK(!tri_rule(12, 4, false, false, false, t1)); // the tuner decides
+    CHECK(tri_rule(12, 4, false, false, false, t1));
+    CHECK(!tri_rule(16, 4, false, false, false, t1)); // the tuner decides
     CHECK(!tri_rule(4, 2, true, false, false, t1));   // Split layout: realigning kernel
     CHECK(!tri_rule(6, 3, false, true, false, t1));   // written + Verify rows: early compares
     CHECK(!tri_rule(10, 9, false, false, false, t1)); // 16-byte entries
     CHECK(!tri_rule(4, 2, false, false, false, tps_of(16 * MiB)));
-    CHECK(tri_tunable(12, 4, false, false, false) && !tri_tunable(16, 4, false, false, false));
+    CHECK(tri_tunable(16, 4, false, false, false) && !tri_tunable(20, 4, false, false, false));
     CHECK(tri_order(TileOrder::kGroup8) == TileOrder::kXcd32);
     CHECK(tri_order(TileOrder::kGroup2) == TileOrder::kGroup2);
     CHECK(tri_order(TileOrder::kConsecutive) == TileOrder::kConsecutive);

@@ -1181,7 +1181,7 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
     assert len(names) == max(1, -(-m // 16))
     plain = {"consecutive", "g8", "g2", "q8", "q16", "x8", "x32"}
     # an encode plan with R <= 8 rows and 3..12 inputs may also take the triple loads
-    tri_ok = 3 <= k <= 12 and m <= 8
+    tri_ok = 3 <= k <= 16 and m <= 8
     allowed = plain | ({"tri", "tri-g2", "tri-x32"} if tri_ok else set())
     assert all(n in allowed for n in names), names
     sb.fill_random(S + k + 1)  # fresh data: the tuned plan must compute it, not reuse
