@@ -131,13 +131,19 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
 
 // Triple-load form of an aligned R <= 8 LDS launch (Policy::WIX 2, rs_kernels.hip
 // takes_tri; DESIGN.md §5 "Shard triples"): the loads of three input shards issued
-// together, then their nibble lookups. Taken for 4 <= K <= 12 up to 8 MiB shards (tps <=
-// 1024) by launches that write every row or compare every row; launches that mix written
+// together, then their nibble lookups. Taken for 4 <= K <= 12 (shard sizes below) by
+// launches that write every row or compare every row; launches that mix written
 // and Verify rows keep the ring of three with its early compare loads (one-erasure decodes
 // ran 0.3-1.5 points slower in triples). RS(12,4) 77.2 -> 80.3 in G2; RS(16,4) gained 0.7
 // there and is left to rs_plan_tune.
+// Shard size bounds it (tools/profile_sweep.sh, profiles/r03/r03s5/profile_sweep.txt, the
+// first rule at tps <= 1024): above 2 MiB shards it lost 1-14 points (RS(8,8) 8 MiB 71.5
+// -> 57.2, RS(8,4) 8 MiB 73.5 -> 67.1, RS(12,4) 5.6 MB 72.5 -> 68.5, RS(6,3) 2.8 MB -1.5),
+// and at shards up to 256 KiB it helped only with few inputs (RS(4,2) 256 KiB 74.4 ->
+// 78.2; RS(10,4) 105 KB 71 -> 68.5). So: 256 KiB < S <= 2 MiB, or S <= 256 KiB with K <= 6.
 inline bool tri_rule(int K, int R, bool misaligned, bool verify, bool read_only, uint64_t tps) {
-  return R <= 8 && K >= 4 && K <= 12 && !misaligned && (!verify || read_only) && tps <= 1024;
+  return R <= 8 && K >= 4 && K <= 12 && !misaligned && (!verify || read_only) &&
+         (tps <= 32 ? K <= 6 : tps <= 256);
 }
 // rs_plan_tune also times the triple form up to K = 16
 inline bool tri_tunable(int K, int R, bool misaligned, bool verify, bool read_only) {

@@ -301,6 +301,10 @@ int main() {
     CHECK(!tri_rule(6, 3, false, true, false, t1));   // written + Verify rows: early compares
     CHECK(!tri_rule(10, 9, false, false, false, t1)); // 16-byte entries
     CHECK(!tri_rule(4, 2, false, false, false, tps_of(16 * MiB)));
+    CHECK(!tri_rule(8, 8, false, false, false, tps_of(8 * MiB)));     // 8 MiB shards: lost
+    CHECK(tri_rule(8, 4, false, false, false, tps_of(2 * MiB)));      // 2 MiB: gained
+    CHECK(tri_rule(4, 2, false, false, false, tps_of(256 << 10)));    // small S, few inputs
+    CHECK(!tri_rule(10, 4, false, false, false, tps_of(104858)));     // small S, 10 inputs
     CHECK(tri_tunable(16, 4, false, false, false) && !tri_tunable(20, 4, false, false, false));
     CHECK(tri_order(TileOrder::kGroup8) == TileOrder::kXcd32);
     CHECK(tri_order(TileOrder::kGroup2) == TileOrder::kGroup2);
