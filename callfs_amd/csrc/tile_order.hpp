@@ -136,14 +136,18 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
 // and Verify rows keep the ring of three with its early compare loads (one-erasure decodes
 // ran 0.3-1.5 points slower in triples). RS(12,4) 77.2 -> 80.3 in G2; RS(16,4) gained 0.7
 // there and is left to rs_plan_tune.
-// Shard size bounds it (tools/profile_sweep.sh, profiles/r03/r03s5/profile_sweep.txt, the
-// first rule at tps <= 1024): above 2 MiB shards it lost 1-14 points (RS(8,8) 8 MiB 71.5
-// -> 57.2, RS(8,4) 8 MiB 73.5 -> 67.1, RS(12,4) 5.6 MB 72.5 -> 68.5, RS(6,3) 2.8 MB -1.5),
-// and at shards up to 256 KiB it helped only with few inputs (RS(4,2) 256 KiB 74.4 ->
-// 78.2; RS(10,4) 105 KB 71 -> 68.5). So: 256 KiB < S <= 2 MiB, or S <= 256 KiB with K <= 6.
+// Shard size bounds it. tools/profile_sweep.sh, the same box with the triple form
+// (profiles/r03/r03s5/profile_sweep.txt, taken up to 8 MiB shards) and without it above 2
+// MiB / at small S for K > 6 (profiles/r03/r03s6/profile_sweep.txt), % of 8 TB/s,
+// ring of three -> triples: RS(8,8) 8 MiB 71.7 -> 57.2, RS(8,4) 8 MiB 74.4 -> 67.1,
+// RS(12,4) 5.6 MB 74.8 -> 68.5, RS(10,4) 6.7 MB 74.2 -> 72.0, but RS(4,2) 4 MiB 69.6 ->
+// 78.4 and RS(6,3) 2.8 MB 72.4 -> 74.2; at small S RS(10,4) 105 KB 71.9 -> 68.5, RS(10,8)
+// 105 KB 65.2 -> 68.5, RS(4,2) 256 KiB 74.4 -> 78.2, RS(8,8) 128 KiB equal. So: S <= 2 MiB
+// (tps <= 256), or up to 4 MiB with K <= 6; at S <= 256 KiB only K <= 6 or R >= 5.
 inline bool tri_rule(int K, int R, bool misaligned, bool verify, bool read_only, uint64_t tps) {
-  return R <= 8 && K >= 4 && K <= 12 && !misaligned && (!verify || read_only) &&
-         (tps <= 32 ? K <= 6 : tps <= 256);
+  if (R > 8 || K < 4 || K > 12 || misaligned || (verify && !read_only)) return false;
+  if (tps <= 32) return K <= 6 || R >= 5;
+  return tps <= 256 || (tps <= 512 && K <= 6);
 }
 // rs_plan_tune also times the triple form up to K = 16
 inline bool tri_tunable(int K, int R, bool misaligned, bool verify, bool read_only) {

@@ -305,6 +305,10 @@ int main() {
     CHECK(tri_rule(8, 4, false, false, false, tps_of(2 * MiB)));      // 2 MiB: gained
     CHECK(tri_rule(4, 2, false, false, false, tps_of(256 << 10)));    // small S, few inputs
     CHECK(!tri_rule(10, 4, false, false, false, tps_of(104858)));     // small S, 10 inputs
+    CHECK(tri_rule(10, 8, false, false, false, tps_of(104858)));      // small S, R = 8
+    CHECK(tri_rule(4, 2, false, false, false, tps_of(4 * MiB)));      // 4 MiB, few inputs
+    CHECK(!tri_rule(10, 4, false, false, false, tps_of(4 * MiB)));
+    CHECK(!tri_rule(10, 4, false, false, false, tps_of(6710887)));    // configs[2] shards
     CHECK(tri_tunable(16, 4, false, false, false) && !tri_tunable(20, 4, false, false, false));
     CHECK(tri_order(TileOrder::kGroup8) == TileOrder::kXcd32);
     CHECK(tri_order(TileOrder::kGroup2) == TileOrder::kGroup2);
