@@ -111,9 +111,10 @@ struct Policy {
   // entries (built in LDS from the nibble tables) instead of six nibble lookups; Verify
   // rows load their compared vectors after the input loop
   // (WIX 2, A/B probe: the same triple loop with the nibble lookups, any R <= 8)
+  // (WIX 2 with REALIGN: the realigning kernel's aligned loads issued in triples)
   static constexpr int WIX = WIX_;
-  static_assert(!WIX_ || (REALIGN_ == 0 && RING_ == 0 && VPF_ == 0 && !NOMATH_ && !SDWA_),
-                "WIX: plain ring-of-three encode kernel only");
+  static_assert(!WIX_ || ((REALIGN_ == 0 || WIX_ == 2) && RING_ == 0 && VPF_ == 0 && !NOMATH_ && !SDWA_),
+                "WIX: ring-of-three kernel only; 6-bit lookups on aligned shards only");
   // > 0: Verify rows' stored vectors are loaded VPF shards before the end of the input
   // loop instead of after it (R <= 4, plain loads, ring of three only)
   static constexpr int VPF = VPF_;
@@ -395,6 +396,29 @@ __device__ __forceinline__ uint4 shift_from_next(const uint4& A, uint32_t d) {
 // Vector v of shard p from this lane's aligned A[v] and the next lane's A[v+1].
 __device__ __forceinline__ uint4 realign(const uint8_t* p, const uint4& A) {
   return shift_from_next(A, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u);
+}
+
+// shift_from_next without branches: the dword shift d >> 2 by two rounds of selects on
+// wave-uniform conditions, the byte shift by v_alignbyte (alignbyte(hi, lo, 0) = lo, so
+// d = 0 needs no case). For loops that realign several shards per iteration (the triple
+// loads): three branchy realigns per iteration took the kernel to 202 VGPRs.
+__device__ __forceinline__ uint4 shift_from_next_sel(const uint4& A, uint32_t d) {
+  const uint32_t s[8] = {A.x, A.y, A.z, A.w, from_next_lane(A.x), from_next_lane(A.y),
+                         from_next_lane(A.z), from_next_lane(A.w)};
+  // v_perm byte selects, not C selects: LLVM folds `c ? s[k + 1] : s[k]` into an indexed
+  // load of s, which it places in scratch
+  const uint32_t sel1 = d & 4u ? 0x07060504u : 0x03020100u, sel2 = d & 8u ? 0x07060504u : 0x03020100u;
+  uint32_t u[7], t[5];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) u[k] = __builtin_amdgcn_perm(s[k + 1], s[k], sel1);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) t[j] = __builtin_amdgcn_perm(u[j + 2], u[j], sel2);
+  const uint32_t r = d & 3u;
+  return make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r), __builtin_amdgcn_alignbyte(t[2], t[1], r),
+                    __builtin_amdgcn_alignbyte(t[3], t[2], r), __builtin_amdgcn_alignbyte(t[4], t[3], r));
+}
+__device__ __forceinline__ uint4 realign_sel(const uint8_t* p, const uint4& A) {
+  return shift_from_next_sel(A, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u);
 }
 
 // ---- aligned parity stores of misaligned rows (Policy::REALIGN == 2) -----------------
@@ -780,15 +804,39 @@ void rs_apply_lds(ApplyArgs a) {
 
     if constexpr (P::REALIGN) {
       static_assert(!P::NOMATH, "REALIGN: no NOMATH form");
-      // ring of three aligned vectors, realigned when consumed
       auto lda = [&](int i) { return ld_aligned<P>(in[i], v0, a.nvec); };
-      uint4 x0 = lda(0), x1 = K > 1 ? lda(1) : x0, x2 = x0;
+      if constexpr (P::WIX == 2) {
+        // triples of aligned loads (as the aligned triple loop below): the next triple's
+        // three loads in flight while one is realigned and looked up
+        const int KT = K / 3;
+        uint4 x0 = lda(0), x1 = K > 1 ? lda(1) : x0, x2 = K > 2 ? lda(2) : x0;
 #pragma unroll 1
-      for (int i = 0; i < K; ++i) {
-        if (i + 2 < K) x2 = lda(i + 2);
-        lds_mac<RT, P::SDWA>(acc, realign(in[i], x0), lds0 + static_cast<uint32_t>(i) * 32u * W);
-        x0 = x1;
-        x1 = x2;
+        for (int g = 0; g < KT; ++g) {
+          const int i = 3 * g + 3;
+          const uint4 n0 = i < K ? lda(i) : x0, n1 = i + 1 < K ? lda(i + 1) : x0,
+                      n2 = i + 2 < K ? lda(i + 2) : x0;
+          const uint32_t b = lds0 + static_cast<uint32_t>(3 * g) * 32u * W;
+          lds_mac<RT>(acc, realign_sel(in[3 * g], x0), b);
+          lds_mac<RT>(acc, realign_sel(in[3 * g + 1], x1), b + 32u * W);
+          lds_mac<RT>(acc, realign_sel(in[3 * g + 2], x2), b + 64u * W);
+          x0 = n0;
+          x1 = n1;
+          x2 = n2;
+        }
+        if (3 * KT < K)
+          lds_mac<RT>(acc, realign_sel(in[3 * KT], x0), lds0 + static_cast<uint32_t>(3 * KT) * 32u * W);
+        if (3 * KT + 1 < K)
+          lds_mac<RT>(acc, realign_sel(in[3 * KT + 1], x1), lds0 + static_cast<uint32_t>(3 * KT + 1) * 32u * W);
+      } else {
+        // ring of three aligned vectors, realigned when consumed
+        uint4 x0 = lda(0), x1 = K > 1 ? lda(1) : x0, x2 = x0;
+#pragma unroll 1
+        for (int i = 0; i < K; ++i) {
+          if (i + 2 < K) x2 = lda(i + 2);
+          lds_mac<RT, P::SDWA>(acc, realign(in[i], x0), lds0 + static_cast<uint32_t>(i) * 32u * W);
+          x0 = x1;
+          x1 = x2;
+        }
       }
     } else if constexpr (P::WIX) {
       // triples: the next triple's three loads are in flight while one is consumed; the
@@ -1097,14 +1145,17 @@ __device__ __forceinline__ void small_vector(const SmallArgs& a, uint32_t v) {
 
 // The completion flag (SmallArgs::done): the host spins on it instead of waiting for the
 // runtime's completion signal, which returned ~5 us after the kernel had ended
-// (tools/small_trace.sh). Every block makes its stores visible system-wide, then counts
-// itself done on a device-memory counter; the last block resets the counter and releases
-// the call's sequence number into the host flag.
+// (tools/small_trace.sh). Every thread makes its own stores visible system-wide (a
+// system-scope release per wave: the workgroup-scope release in __syncthreads does not wait
+// for another wave's PCIe stores), then the block counts itself done on a device-memory
+// counter; the last block resets the counter and releases the call's sequence number into
+// the host flag.
 template <int RT>
 __global__ __launch_bounds__(256) void rs_apply_small(SmallArgs a) {
   const uint32_t v = blockIdx.x * 256u + threadIdx.x;
   if (v < a.nvec) small_vector<RT>(a, v);
   if (a.done) {  // launch-uniform
+    __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence_system();

@@ -310,7 +310,11 @@ bool spin_until(const int* flag, int want, int us) {
     if ((i & 63u) == 63u &&
         std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(us))
       return false;
+#if defined(__x86_64__) || defined(__i386__)
     __builtin_ia32_pause();
+#else
+    std::this_thread::yield();
+#endif
   }
 }
 
@@ -1591,6 +1595,15 @@ int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
   return RS_OK;
 }
 
+// A timed launch that dispatches no kernel still records both events on the stream, so
+// the caller's elapsed time is this launch's (zero), never a stale earlier interval.
+static int record_empty(void* stream, void* start_event, void* stop_event) {
+  const auto s = static_cast<hipStream_t>(stream);
+  if (start_event) HIPCHK(hipEventRecord(static_cast<hipEvent_t>(start_event), s));
+  if (stop_event) HIPCHK(hipEventRecord(static_cast<hipEvent_t>(stop_event), s));
+  return RS_OK;
+}
+
 int rs_plan_launch(rs_plan* plan, void* stream) {
   return rs_plan_launch_timed(plan, stream, nullptr, nullptr);
 }
@@ -1604,6 +1617,8 @@ int rs_plan_launch_timed(rs_plan* plan, void* stream, void* start_event, void* s
     std::lock_guard<std::mutex> g(plan->mu);
     orders = plan->orders;
   }
+  if (plan->S == 0)  // nothing dispatches: the events still bracket this (empty) launch
+    return record_empty(stream, start_event, stop_event);
   LaunchEvents ev;
   ev.start = static_cast<hipEvent_t>(start_event);
   ev.stop = static_cast<hipEvent_t>(stop_event);
@@ -1628,6 +1643,8 @@ int rs_plan_launch_ceiling_timed(rs_plan* plan, void* stream, int mode, void* st
     std::lock_guard<std::mutex> g(plan->mu);
     orders = plan->orders;
   }
+  if (plan->S < 16)  // the ceilings cover whole 16-B vectors only: nothing dispatches
+    return record_empty(stream, start_event, stop_event);
   const Tables& t = *plan->tables;
   auto* d = static_cast<uint8_t*>(plan->dmeta);
   const size_t ng = t.groups.size();

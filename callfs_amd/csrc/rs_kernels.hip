@@ -91,6 +91,11 @@ using LdsWixPolicy = dev::Policy<8, 1, true, true, false, 512, 2, ORD, 0, false,
 // with nibble lookups, R <= 8
 template <int R, int ORD>
 using LdsTriPolicy = dev::Policy<(R <= 4 ? 8 : 2), 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, 2>;
+// The realigning kernel with its aligned loads issued in triples (rs_apply.hpp REALIGN
+// with WIX 2)
+template <int R, int ORD>
+using LdsRealignTriPolicy =
+    dev::Policy<(R <= 4 ? 7 : 2), 1, true, true, false, 512, 2, ORD, 0, false, 2, false, 0, 0, 2>;
 template <int ORD>
 using LdsRealignOutPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 2>;
 template <int ORD>
@@ -238,11 +243,22 @@ template <int ORD, int... Rs>
 constexpr auto lds_tri_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsTriPolicy<Rs + 1, ORD>>...};
 }
-// [consecutive, G2, X32][R - 1]
-const std::array<std::array<VecFn, 8>, 3> kLdsTri = {
+// [consecutive, G2, X32, Q8, Q16][R - 1] (tri_index)
+const std::array<std::array<VecFn, 8>, 5> kLdsTri = {
     lds_tri_table<0>(std::make_integer_sequence<int, 8>{}),
     lds_tri_table<5>(std::make_integer_sequence<int, 8>{}),
-    lds_tri_table<11>(std::make_integer_sequence<int, 8>{})};
+    lds_tri_table<11>(std::make_integer_sequence<int, 8>{}),
+    lds_tri_table<6>(std::make_integer_sequence<int, 8>{}),
+    lds_tri_table<8>(std::make_integer_sequence<int, 8>{})};
+template <int ORD, int... Rs>
+constexpr auto lds_realign_tri_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignTriPolicy<Rs + 1, ORD>>...};
+}
+// [consecutive, X8, X32][R - 1]
+const std::array<std::array<VecFn, 8>, 3> kLdsRealignTri = {
+    lds_realign_tri_table<0>(std::make_integer_sequence<int, 8>{}),
+    lds_realign_tri_table<10>(std::make_integer_sequence<int, 8>{}),
+    lds_realign_tri_table<11>(std::make_integer_sequence<int, 8>{})};
 template <int ORD, int... Rs>
 constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1, ORD>>...};
@@ -376,9 +392,26 @@ bool tri_tunable_launch(const ApplyArgs& a) {
   return wix_enabled() && tri_tunable(a.K, a.R, (a.in_misalign | a.out_misalign) != 0,
                                       (a.verify_mask & rows) != 0, (a.verify_mask & rows) == rows);
 }
-int tri_index(TileOrder o) { return o == TileOrder::kGroup2 ? 1 : o == TileOrder::kXcd32 ? 2 : 0; }
+// kLdsTri's first index; orders without a triple instance (G8, X8) are not offered
+int tri_index(TileOrder o) {
+  switch (o) {
+    case TileOrder::kGroup2: return 1;
+    case TileOrder::kXcd32: return 2;
+    case TileOrder::kSeg8: return 3;
+    case TileOrder::kSeg16: return 4;
+    default: return 0;
+  }
+}
 bool takes_realign(const ApplyArgs& a) {
   return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u);
+}
+
+// The rule's realigning launches with triple loads (tile_order.hpp realign_tri_rule);
+// CALLFS_RS_WIX=0 keeps them on the ring of three
+bool takes_realign_tri(const ApplyArgs& a) {
+  const uint32_t rows = (1u << a.R) - 1;
+  return wix_enabled() && realign_tri_rule(a.K, a.R, (a.verify_mask & rows) != 0,
+                                           (a.verify_mask & rows) == rows);
 }
 
 // The realigning kernel's tile order (index into kLdsRealignOut): a tuned realign code
@@ -415,10 +448,17 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
     const auto realign_in = [](TileOrder o) {
       return static_cast<TileOrder>(kOrderRealign + static_cast<int>(o));
     };
+    const auto rtri_in = [](TileOrder o) {
+      return static_cast<TileOrder>(kOrderRealignTri + static_cast<int>(o));
+    };
     const auto wix_in = [](TileOrder o) {
       return static_cast<TileOrder>(kOrderWix + static_cast<int>(o));
     };
-    if (takes_realign(a)) add(realign_in(TileOrder::kXcd32));
+    // the rule's kernel first (rs_plan_tune's bar favours cand[0]): the realign order the
+    // rule itself runs (realign_order_index(-1) follows CALLFS_RS_TILE_ORDER)
+    static constexpr TileOrder kRealignRule[3] = {TileOrder::kConsecutive, TileOrder::kXcd8,
+                                                  TileOrder::kXcd32};
+    if (takes_realign(a)) add(realign_in(kRealignRule[realign_order_index(-1)]));
     const auto tri_in = [](TileOrder o) {
       return static_cast<TileOrder>(kOrderTri + static_cast<int>(o));
     };
@@ -428,6 +468,11 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(realign_in(TileOrder::kXcd32));
       add(realign_in(TileOrder::kConsecutive));
       if (every_instance) add(realign_in(TileOrder::kXcd8));
+      if (a.K >= 3) {  // the realigning kernel with triple loads
+        add(rtri_in(TileOrder::kXcd32));
+        add(rtri_in(TileOrder::kConsecutive));
+        if (every_instance) add(rtri_in(TileOrder::kXcd8));
+      }
     }
     add(TileOrder::kConsecutive);
     add(TileOrder::kGroup2);
@@ -445,6 +490,10 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(tri_in(TileOrder::kConsecutive));
       add(tri_in(TileOrder::kGroup2));
       add(tri_in(TileOrder::kXcd32));
+      if (tps > 1024) {
+        add(tri_in(TileOrder::kSeg8));
+        add(tri_in(TileOrder::kSeg16));
+      }
     }
     if (every_instance && can_wix(a)) {  // WIX: A/B instances only
       const int n0 = static_cast<int>(c.size());
@@ -465,6 +514,9 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
+  // realigning kernel with triple loads: kOrderRealignTri + its order -> kOrderRealign + it
+  const bool rtri = order >= kOrderRealignTri && a.K >= 3 && can_realign(a);
+  if (order >= kOrderRealignTri) order = rtri ? order - kOrderRealignTri + kOrderRealign : -1;
   bool tri = order >= kOrderTri && a.R <= 8 && a.K >= 3;
   if (order >= kOrderTri) order = tri ? order - kOrderTri : -1;
   const bool wix = order >= kOrderWix && can_wix(a);
@@ -528,7 +580,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         // misaligned shards: the realigning form, unless a tuned order names a plain kernel
         if (can_realign(a) && (order >= kOrderRealign || (order < 0 && takes_realign(a)))) {
-          fn = kLdsRealignOut[realign_order_index(order)][a.R - 1];
+          fn = (rtri || (order < 0 && takes_realign_tri(a)) ? kLdsRealignTri : kLdsRealignOut)
+              [realign_order_index(order)][a.R - 1];
           gx = dev::vec_grid<LdsRealignOutPolicy<0>>(a.nvec, a.batch);
           a.tail_in_vec = 1;  // its first tile writes every edge byte, the tail included
           tail0 = a.S;
@@ -625,7 +678,8 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
   a.tail_in_vec = a.nvec * 16 < a.S;
-  if (order >= kOrderTri) order -= kOrderTri;
+  if (order >= kOrderRealignTri) order = order - kOrderRealignTri + kOrderRealign;
+  else if (order >= kOrderTri) order -= kOrderTri;
   if (order >= kOrderWix) order -= kOrderWix;  // bounded by the nibble kernel's traffic
   // the order the production launch would take (a tuned order, else the rule; the
   // realigning and v_perm launches are bounded by the plain kernel's traffic)

@@ -108,8 +108,11 @@ constexpr int kOrderRealign = 32;
 // (kOrderWix + a TileOrder: the R <= 4 LDS kernel with 6-bit lookups over shard triples,
 // rs_apply.hpp Policy::WIX; aligned launches without Verify rows, K >= 3)
 constexpr int kOrderWix = 64;
-// (kOrderTri + consecutive / G2 / X32: A/B probe, the triple loop with nibble lookups)
+// (kOrderTri + consecutive / G2 / X32 / Q8 / Q16: the triple loop with nibble lookups)
 constexpr int kOrderTri = 96;
+// (kOrderRealignTri + consecutive / X8 / X32: the realigning kernel with its aligned loads
+// issued in triples)
+constexpr int kOrderRealignTri = 128;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the

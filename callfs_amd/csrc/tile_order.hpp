@@ -149,6 +149,13 @@ inline bool tri_rule(int K, int R, bool misaligned, bool verify, bool read_only,
   if (tps <= 32) return K <= 6 || R >= 5;
   return tps <= 256 || (tps <= 512 && K <= 6);
 }
+// Triple loads in the realigning kernel (misaligned shards, upstream Split layout):
+// measured in round 4 (DESIGN.md §5 "Shard triples"); until then only rs_plan_tune and
+// rs_plan_set_orders take it.
+inline bool realign_tri_rule(int K, int R, bool verify, bool read_only) {
+  (void)K; (void)R; (void)verify; (void)read_only;
+  return false;
+}
 // rs_plan_tune also times the triple form up to K = 16
 inline bool tri_tunable(int K, int R, bool misaligned, bool verify, bool read_only) {
   return R <= 8 && K >= 3 && K <= 16 && !misaligned && (!verify || read_only);

@@ -1126,13 +1126,15 @@ def test_host_pool_reuses_freed_buffers(native_lib):
     (10, 4, 16 * 1000, 2, 3),          # S % 16 == 0, every shard misaligned by 3
     (8, 3, 16 * 496 * 3 + 7, 2, 8),    # R = 3, three tiles
 ])
-def test_plan_misaligned_batch_realign(native_lib, k, m, S, batch, off):
+@pytest.mark.parametrize("form", ["rule", "realign-x32", "realign-tri-x32", "realign-tri"])
+def test_plan_misaligned_batch_realign(native_lib, k, m, S, batch, off, form):
     """Contiguous stripes in the upstream Split layout at odd S (every input shard at its
     own byte misalignment, odd stripe stride): k >= 8 launches take the realigning LDS
     kernel (aligned loads, DPP + v_alignbyte), and with misaligned parity rows its form
     that also aligns the stores (62 vectors per wave, edge bytes in the first tile). Encode,
     a decode erasing m shards, and a decode with Verify rows, against the oracle per
-    stripe, every byte of every stripe."""
+    stripe, every byte of every stripe. `form` pins the realigning kernel's ring-of-three
+    or triple-load instance (rs_plan_set_orders) instead of the rule's."""
     import torch
     from callfs_amd.device import Plan
     n = k + m
@@ -1140,7 +1142,14 @@ def test_plan_misaligned_batch_realign(native_lib, k, m, S, batch, off):
     buf = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device="cuda:0")
     base = buf.data_ptr() + off
     ptrs = [base + (b * n + i) * S for b in range(batch) for i in range(n)]
-    Plan(k, m, S, batch, ptrs).launch()
+
+    def pinned(plan):
+        if form != "rule":
+            plan.set_orders([form] * int(N.lib.rs_plan_groups(plan.handle)))
+        return plan
+
+    from callfs_amd import _native as N
+    pinned(Plan(k, m, S, batch, ptrs)).launch()
     torch.cuda.synchronize()
     host = buf.cpu().numpy()[off:off + total].copy()
     for b in range(batch):
@@ -1153,7 +1162,7 @@ def test_plan_misaligned_batch_realign(native_lib, k, m, S, batch, off):
             for i in erase:
                 s0 = off + (b * n + i) * S
                 buf[s0:s0 + S].zero_()
-        dec = Plan(k, m, S, batch, ptrs, present=[i not in erase for i in range(n)])
+        dec = pinned(Plan(k, m, S, batch, ptrs, present=[i not in erase for i in range(n)]))
         dec.launch()
         assert not dec.corrupt(), erase
         assert np.array_equal(buf.cpu().numpy()[off:off + total], host), erase
@@ -1182,7 +1191,7 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
     plain = {"consecutive", "g8", "g2", "q8", "q16", "x8", "x32"}
     # an encode plan with R <= 8 rows and 3..12 inputs may also take the triple loads
     tri_ok = 3 <= k <= 16 and m <= 8
-    allowed = plain | ({"tri", "tri-g2", "tri-x32"} if tri_ok else set())
+    allowed = plain | ({"tri", "tri-g2", "tri-x32", "tri-q8", "tri-q16"} if tri_ok else set())
     assert all(n in allowed for n in names), names
     sb.fill_random(S + k + 1)  # fresh data: the tuned plan must compute it, not reuse
     enc.launch()
@@ -1213,7 +1222,8 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
 
 ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign",
                    "realign-x8", "realign-x32", "wix", "wix-g8", "wix-g2", "wix-q8", "wix-q16",
-                   "wix-x8", "wix-x32", "tri", "tri-g2", "tri-x32"]
+                   "wix-x8", "wix-x32", "tri", "tri-g2", "tri-x32", "tri-q8", "tri-q16",
+                   "realign-tri", "realign-tri-x8", "realign-tri-x32"]
 
 
 @pytest.mark.parametrize("k,m,S,batch,off,erase", [
@@ -1223,6 +1233,8 @@ ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign
     (6, 3, (1 << 18) + 32, 3, 0, (2,)),    # aligned, 1 written + 2 Verify rows (WIX too)
     (10, 8, 300_001, 5, 3, None),          # R = 8, realigning kernel
     (4, 2, 8 * 512 * 16 * 9 + 7, 2, 0, (0, 1)),  # k = 4, R = 2 decode, ragged tail
+    (4, 2, (8 << 20) + 8192 * 3 + 16, 2, 0, None),  # > 1024 tiles per stripe: Q8 / Q16
+    (5, 3, (8 << 20) + 1, 2, 1, None),     # Split layout, K = 5: realigning triple + 2
 ])
 def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, erase):
     """rs_plan_set_orders pins each tile order the launch group's kernel offers (the
@@ -1270,8 +1282,11 @@ def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, era
             assert plan.corrupt_stripes() == [1], name
     assert "consecutive" in taken or "realign" in taken, taken
     if (off | S) % 2:  # shards at odd offsets
-        assert {"realign", "realign-x8", "realign-x32"} <= set(taken), taken
+        assert {"realign", "realign-x8", "realign-x32", "realign-tri", "realign-tri-x8",
+                "realign-tri-x32"} <= set(taken), taken
     else:
+        if S // 8192 > 1024 and m <= 8:  # tiles per stripe: triple loads in segment orders
+            assert {"tri-q8", "tri-q16"} <= set(taken), taken
         assert {"x8", "x32"} <= set(taken), taken
         with pytest.raises(N.NativeError):
             plan.set_orders(["realign"])  # aligned shards: no realigning kernel
@@ -1550,3 +1565,25 @@ def test_small_path_verify_masks_the_tail_vector(codec, k, m, L):
         sh = [None if i == 0 else bad[i] for i in range(k + m)]
         with pytest.raises(ErrShardCorrupted):
             codec.decode(sh, p, L)
+
+
+@pytest.mark.parametrize("k,m,S,B", [(10, 4, 960, 150),    # 150 blocks in y, one in x
+                                     (10, 4, 16000, 9),    # 4 x 9 blocks
+                                     (4, 2, 340_000, 1),   # 84 blocks, one stripe
+                                     (16, 4, 6000, 16)])   # 2 x 16 blocks, 2 loads rounds
+def test_small_path_every_byte_right_after_flag(native_lib, k, m, S, B):
+    """One-dispatch calls of close to the 2 MiB staging limit spread over many blocks: the
+    host reads outputs as soon as the kernel's completion flag is released, so every
+    block's (every wave's) PCIe stores must be visible by then. Repeated back to back,
+    every byte of every stripe checked against the oracle."""
+    from callfs_amd import erasure as E
+    assert ((S + 15) // 16 * 16) * (k + m) * B <= 2 << 20  # one dispatch
+    rng = np.random.default_rng(S * B + k)
+    for rep in range(6):
+        stripes = [[rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] for _ in range(B)]
+        parity, status = E.encode_batch(stripes, k, m)
+        assert status == [0] * B
+        for b in range(B):
+            want = cref.encode(stripes[b], k, m)
+            for j in range(m):
+                assert bytes(parity[b][j]) == bytes(want[j]), (rep, b, j)

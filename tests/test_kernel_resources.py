@@ -70,7 +70,10 @@ def test_lds_kernel_occupancy(kernels):
         r = int(re.search(r"rs_apply_lds<(\d+),", k["name"]).group(1))
         realign = _policy(k)[10] not in ("false", "0")
         triple = _policy(k)[14] == "2"  # triple loads: 12 more VGPRs, measured at 5 waves
-        want = 8 if r <= 4 else (6 if realign else 5 if triple else 7) if r <= 8 else 4
+        if realign and triple:  # realigning triples: 67 VGPRs at R <= 4, 94 at R 5..8
+            want = 7 if r <= 4 else 5
+        else:
+            want = 8 if r <= 4 else (6 if realign else 5 if triple else 7) if r <= 8 else 4
         assert k["waves_per_simd"] >= want, (k["name"], k["vgprs"], k["waves_per_simd"])
         if r > 8:
             assert k["vgprs"] + k.get("agprs", 0) <= 128, k["name"]
