@@ -75,7 +75,7 @@ using LdsVerifyPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, fal
 // addresses realigned the same way (62 vectors per wave; the bytes no aligned block
 // covers are written by each stripe's first tile; rs_apply.hpp REALIGN 2). Round 1's
 // form realigned only the loads (REALIGN 1, 63 vectors per wave, k >= 8; kept in
-// tools/kbench for comparison). tools/realign_out_sweep.sh, tools/wave_tiling_probe.sh,
+// tools/kbench for comparison). tools/realign_out_sweep.sh (round 2), tools/wave_tiling_probe.sh,
 // profiles/r02/realign_out/, % of 8 TB/s, unaligned -> loads realigned -> loads and stores
 // realigned: RS(10,4) 64 MiB objects (S = 6,710,887) 67.6 -> 68.1 -> 69.5, RS(10,8)
 // 1,048,577 B 63.9 -> 65.3 -> 67.0, RS(6,3) 65.6 -> 67.0 -> 71.5, RS(5,3) 68.7 -> 66.7
@@ -367,11 +367,11 @@ bool wix_enabled() {
 }
 // Since the triple-load form (below) measured equal or faster than WIX everywhere, the
 // rule no longer takes WIX: its instances remain for rs_plan_set_orders (A/B).
-// tools/wix_ab*.sh, profiles/r03/wix/: WIX in the nibble rule's order vs the nibble kernel's
+// tools/wix_ab*.sh (round 3, since removed), profiles/r03/wix/: WIX in the nibble rule's order vs the nibble kernel's
 // best order, 1 MiB shards: RS(4,2) 72.3 -> 79.0, RS(4,4) 75.0 -> 81.5, RS(5,3) 74.5 -> 79.9,
 // RS(8,4) 76.5 -> 80.1; RS(10,4) equal, RS(16,4) / RS(20,4) / RS(32,4) -1.2 ... -1.5.
 
-// Triple loads (Policy::WIX 2): tile_order.hpp tri_rule. tools/wix_ab4.sh,
+// Triple loads (Policy::WIX 2): tile_order.hpp tri_rule. tools/wix_ab4.sh (round 3, since removed),
 // profiles/r03/wix/ab4_tri_verify.jsonl, % of 8 TB/s, nibble (best order) -> triples in
 // the rule's order: RS(4,2) 71.8 -> 80.6, RS(5,3) 74.6 -> 80.3, RS(8,4) 76.3 -> 80.2,
 // RS(10,4) 75.8 -> 76.6, RS(6,6) 74.6 -> 75.7, RS(8,8) 75.4 -> 76.3, RS(10,8) 74.1 -> 77.4;
@@ -477,7 +477,7 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
     add(TileOrder::kConsecutive);
     add(TileOrder::kGroup2);
     if (tps <= 32) add(TileOrder::kGroup8);
-    if (tps > 1024) {
+    if (tps > 1024 || (every_instance && tps >= 64)) {
       add(TileOrder::kSeg8);
       add(TileOrder::kSeg16);
     }
@@ -490,7 +490,7 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(tri_in(TileOrder::kConsecutive));
       add(tri_in(TileOrder::kGroup2));
       add(tri_in(TileOrder::kXcd32));
-      if (tps > 1024) {
+      if (tps > 1024 || (every_instance && tps >= 64)) {
         add(tri_in(TileOrder::kSeg8));
         add(tri_in(TileOrder::kSeg16));
       }

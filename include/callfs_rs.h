@@ -99,10 +99,12 @@ int rs_codec_decode(rs_ctx* ctx, int k, int m, uint8_t* const* shards, size_t* l
  * bodies and backend shards straight into these buffers. Calls with any
  * other buffer use the copy-pool staging path as before. Free with rs_host_free
  * (RS_E_ARG for a pointer rs_host_alloc did not return or that was already freed).
- * Freed buffers are kept by the context for reuse: a later rs_host_alloc of a similar
- * size (within a quarter of a kept buffer) returns one without page-locking new memory,
- * so a server may allocate a body per request (CALLFS_RS_HOST_POOL_BYTES caps the idle
- * bytes kept, default 8 GiB; rs_shutdown releases them). No reference equivalent: Go's
+ * Freed buffers are kept by the context for reuse: fresh buffers are allocated in 2 MiB
+ * granules, and a later rs_host_alloc returns the smallest kept buffer that fits without
+ * wasting more than a quarter of it, both sides counted in granules (so a 4 KiB body
+ * freed by one request serves the next), without page-locking new memory; a server may
+ * allocate a body per request (CALLFS_RS_HOST_POOL_BYTES caps the idle bytes kept,
+ * default 4 GiB, 0 = keep none; rs_shutdown releases them). No reference equivalent: Go's
  * io.ReadAll allocations (post_file_enhanced.go:127, manager.go:473,530) are what it
  * replaces on a ROCm build. */
 int rs_host_alloc(rs_ctx* ctx, size_t bytes, void** out);
