@@ -90,6 +90,27 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
+def cpu_quota_cores():
+    """CPUs the process's cgroup grants (cgroup v2 cpu.max, else v1 cfs quota/period), or
+    None when unlimited or unreadable: the GPU box's affinity mask lists every host CPU,
+    but its cgroup may grant far fewer."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as fh:
+                txt = fh.read().strip()
+            if parse:
+                q, per = parse(txt)
+                return None if q == "max" else round(int(q) / int(per), 2)
+            q = int(txt)
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                per = int(fh.read().strip())
+            return None if q <= 0 else round(q / per, 2)
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -171,6 +192,15 @@ def cpu_baseline(sb, k, m, erase, seconds, ws_bytes, threads, all_threads=0):
     if extra:
         out["modes"].update(extra)
         out["all_visible_threads"] = min(all_threads, ns, 256)
+        quota = cpu_quota_cores()
+        out["cpu_quota_cores"] = quota
+        out["all_visible_note"] = (
+            f"stripe-parallel at {out['all_visible_threads']} threads (every CPU in the "
+            f"affinity mask, capped by the {ns} sampled stripes): {extra['all-visible']} GiB/s "
+            f"against {modes['stripe-parallel']} at {threads}; cgroup CPU quota "
+            + (f"{quota} CPUs" if quota else "unlimited or unreadable")
+            + ". More threads than the CPUs the box grants time-slice instead of running "
+            "in parallel, so `value` stays the per-GPU share")
     return out
 
 

@@ -113,7 +113,9 @@ struct Policy {
   // (WIX 2, A/B probe: the same triple loop with the nibble lookups, any R <= 8)
   // (WIX 2 with REALIGN: the realigning kernel's aligned loads issued in triples)
   static constexpr int WIX = WIX_;
-  static_assert(!WIX_ || ((REALIGN_ == 0 || WIX_ == 2) && RING_ == 0 && VPF_ == 0 && !NOMATH_ && !SDWA_),
+  // (WIX 2 with VPF: the aligned triple loop with early compare loads)
+  static_assert(!WIX_ || ((REALIGN_ == 0 || WIX_ == 2) && (VPF_ == 0 || (WIX_ == 2 && REALIGN_ == 0)) &&
+                          RING_ == 0 && !NOMATH_ && !SDWA_),
                 "WIX: ring-of-three kernel only; 6-bit lookups on aligned shards only");
   // > 0: Verify rows' stored vectors are loaded VPF shards before the end of the input
   // loop instead of after it (R <= 4, plain loads, ring of three only)
@@ -842,12 +844,23 @@ void rs_apply_lds(ApplyArgs a) {
       // triples: the next triple's three loads are in flight while one is consumed; the
       // K % 3 shards left over take the nibble tables
       const int KT = K / 3;
+      // VPF: the Verify rows' compare loads go out with the triple whose loads reach K - VPF
+      // (or with the last triple when the remainder shards do)
+      const int gv = kVpf ? std::min(KT - 1, (std::max(3, K - P::VPF) - 3) / 3) : -1;
       uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = K > 2 ? ld(2) : x0;
 #pragma unroll 1
       for (int g = 0; g < KT; ++g) {
         const int i = 3 * g + 3;
         const uint4 n0 = i < K ? ld(i) : x0, n1 = i + 1 < K ? ld(i + 1) : x0,
                     n2 = i + 2 < K ? ld(i + 2) : x0;
+        if constexpr (kVpf) {
+          if (g == gv) {
+#pragma unroll
+            for (int r = 0; r < RT; ++r)
+              if (r < R && ((a.verify_mask >> r) & 1u))
+                vpre[r] = load16<P>(reinterpret_cast<const uint4*>(out[r]) + v0);
+          }
+        }
         if constexpr (P::WIX == 1) {
           wix_mac<RT>(acc, x0, x1, x2, lds0 + wix_base(K) + 1024u * static_cast<uint32_t>(g));
         } else {

@@ -91,6 +91,11 @@ using LdsWixPolicy = dev::Policy<8, 1, true, true, false, 512, 2, ORD, 0, false,
 // with nibble lookups, R <= 8
 template <int R, int ORD>
 using LdsTriPolicy = dev::Policy<(R <= 4 ? 8 : 2), 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, 2>;
+// The triple loop with the Verify rows' compare loads issued with the triple that reaches
+// K - 4 (Policy::VPF, as LdsVerifyPolicy): launches of R <= 4 rows that mix written and
+// Verify rows (the one-erasure decode of a download) when they take triples
+template <int ORD>
+using LdsTriVerifyPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 4, 2>;
 // The realigning kernel with its aligned loads issued in triples (rs_apply.hpp REALIGN
 // with WIX 2)
 template <int R, int ORD>
@@ -250,6 +255,13 @@ const std::array<std::array<VecFn, 8>, 5> kLdsTri = {
     lds_tri_table<11>(std::make_integer_sequence<int, 8>{}),
     lds_tri_table<6>(std::make_integer_sequence<int, 8>{}),
     lds_tri_table<8>(std::make_integer_sequence<int, 8>{})};
+// [consecutive, G2, X32, Q8, Q16][R - 1] for R <= 4 with Verify rows (tri_index)
+const std::array<std::array<VecFn, 4>, 5> kLdsTriVerify = {
+    lds_order_table<LdsTriVerifyPolicy<0>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriVerifyPolicy<5>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriVerifyPolicy<11>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriVerifyPolicy<6>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriVerifyPolicy<8>>(std::make_integer_sequence<int, 4>{})};
 template <int ORD, int... Rs>
 constexpr auto lds_realign_tri_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignTriPolicy<Rs + 1, ORD>>...};
@@ -556,7 +568,12 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
             lds = dev::lds_bytes_wix(a.K);
           }
           if (!tri && order < 0 && takes_tri(a)) tri = true;  // the rule: ord is the nibble rule's
-          if (tri) fn = kLdsTri[tri_index(order < 0 ? tri_order(ord) : ord)][a.R - 1];
+          if (tri) {
+            const int ti = tri_index(order < 0 ? tri_order(ord) : ord);
+            fn = a.R <= 4 && (a.verify_mask & rows) && (a.verify_mask & rows) != rows
+                     ? kLdsTriVerify[ti][a.R - 1]  // written + Verify rows: early compares
+                     : kLdsTri[ti][a.R - 1];
+          }
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }

@@ -157,8 +157,10 @@ inline bool realign_tri_rule(int K, int R, bool verify, bool read_only) {
   return false;
 }
 // rs_plan_tune also times the triple form up to K = 16
+// (R <= 4 launches that mix written and Verify rows take the triple loop with early
+// compare loads, Policy::VPF)
 inline bool tri_tunable(int K, int R, bool misaligned, bool verify, bool read_only) {
-  return R <= 8 && K >= 3 && K <= 16 && !misaligned && (!verify || read_only);
+  return R <= 8 && K >= 3 && K <= 16 && !misaligned && (!verify || read_only || R <= 4);
 }
 // The triple form's tile order (instances: consecutive, G2, X32) for the order the nibble
 // rule picks: G8 (shards up to 256 KiB) -> X32, which ran within 0.6 points of G8 for the

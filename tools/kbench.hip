@@ -69,6 +69,70 @@ __global__ __launch_bounds__(256) void xor_stream(ApplyArgs a) {
     dev::store16<P>(reinterpret_cast<uint4*>(out[r]) + v, make_uint4(acc.x + r, acc.y, acc.z, acc.w));
 }
 
+
+// Hybrid row split (VERDICT r03 item 3 probe): rows 0..RL-1 of a wide launch group take the
+// LDS nibble tables with 8-byte entries (ds_read_b64, 2 LDS-array cycles per lookup where
+// 16-byte entries take 4), rows RL..RL+RV-1 the v_perm products of the k <= 3 kernel
+// (coefficient tables through the constant address space, s_load). Halves the LDS-array
+// cycles of R = 16 and moves the rest onto the VALU. Consecutive tiles, ring of three.
+template <int RL, int RV>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 8)))
+void hybrid_kernel(ApplyArgs a, const uint8_t* ltabs8) {
+  using namespace dev;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int K = a.K;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(ltabs8);
+    uint4* dst = reinterpret_cast<uint4*>(smem);
+    for (int j = threadIdx.x; j < K * 16; j += 512) dst[j] = src[j];
+  }
+  __syncthreads();
+  const uint32_t lds0 = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)smem));
+  const uint32_t tps = static_cast<uint32_t>((a.nvec + 511) / 512);
+  const uint32_t stripe = blockIdx.x / tps, tile = blockIdx.x - stripe * tps;
+  const uint64_t v0 = static_cast<uint64_t>(tile) * 512 + threadIdx.x;
+  if (v0 >= a.nvec) return;
+  cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
+  cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * a.R;
+  const cptr<uint32_t> tabs = as_const(a.tabs);
+  using P = Policy<2, 1, true, true, false, 512>;
+  auto ld = [&](int i) { return load16<P>(reinterpret_cast<const uint4*>(in[i]) + v0); };
+  typename LdsAcc<8>::T accL[4][4];
+  uint32_t accV[RV][4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accL[w][j] = 0;
+#pragma unroll
+    for (int r = 0; r < RV; ++r) accV[r][w] = 0;
+  }
+  uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = x0;
+#pragma unroll 1
+  for (int i = 0; i < K; ++i) {
+    if (i + 2 < K) x2 = ld(i + 2);
+    lds_mac<8>(accL, x0, lds0 + static_cast<uint32_t>(i) * 256u);
+    const cptr<uint32_t> t = tabs + (static_cast<size_t>(i) * a.R + RL) * 5;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const Sel sel = selectors(word(x0, w));
+#pragma unroll
+      for (int r = 0; r < RV; ++r) accV[r][w] = fma1(accV[r][w], gf_mul4(sel, t + r * 5));
+    }
+    x0 = x1;
+    x1 = x2;
+  }
+#pragma unroll
+  for (int r = 0; r < RL; ++r)
+    store16<P>(reinterpret_cast<uint4*>(out[r]) + v0,
+               make_uint4(lds_row<8>(accL[0], r), lds_row<8>(accL[1], r), lds_row<8>(accL[2], r),
+                          lds_row<8>(accL[3], r)));
+#pragma unroll
+  for (int r = 0; r < RV; ++r)
+    store16<P>(reinterpret_cast<uint4*>(out[RL + r]) + v0,
+               make_uint4(accV[r][0], accV[r][1], accV[r][2], accV[r][3]));
+}
+
 template <int R, class P>
 void launch_lds(const ApplyArgs& a, hipStream_t s) {
   const unsigned g = dev::vec_grid<P>(a.nvec, a.batch);
@@ -233,6 +297,18 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(d_out, out.data(), out.size() * sizeof(void*), hipMemcpyHostToDevice));
   CK(hipMemcpy(d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemset(d_status, 0, 4));
+  // KB_HYBRID: 8-byte nibble tables of rows 0..7 (hybrid_kernel's LDS rows)
+  static void* d_ltabs8 = nullptr;
+  if (m > 8) {
+    std::vector<uint8_t> l8(static_cast<size_t>(k) * 256);
+    for (int i = 0; i < k; ++i) {
+      uint8_t col[8];
+      for (int r = 0; r < 8; ++r) col[r] = E.at(k + r, i);
+      nibble_tables(col, 8, &l8[static_cast<size_t>(i) * 256]);
+    }
+    CK(hipMalloc(&d_ltabs8, l8.size()));
+    CK(hipMemcpy(d_ltabs8, l8.data(), l8.size(), hipMemcpyHostToDevice));
+  }
 
   ApplyArgs a{};
   a.in_tab = static_cast<const uint8_t* const*>(d_in);
@@ -467,6 +543,20 @@ int main(int argc, char** argv) {
     vs.push_back(Variant{"perm g2", [m](const ApplyArgs& a, hipStream_t s) { pm_g2[m - 1](a, s); }});
     vs.push_back(Variant{"sdwa consec", [m](const ApplyArgs& a, hipStream_t s) { sd_c[m - 1](a, s); }});
     vs.push_back(Variant{"perm consec", [m](const ApplyArgs& a, hipStream_t s) { pm_c[m - 1](a, s); }});
+  }
+  if (std::getenv("KB_HYBRID") && (m == 12 || m == 16)) {  // LDS rows 0..7 + v_perm rows 8..m-1
+    auto hv = [](const ApplyArgs& a, hipStream_t s) {
+      const unsigned g = static_cast<unsigned>((a.nvec + 511) / 512 * a.batch);
+      const size_t lds = static_cast<size_t>(a.K) * 256;
+      if (a.R == 16)
+        hipLaunchKernelGGL((hybrid_kernel<8, 8>), dim3(g), dim3(512), lds, s, a,
+                           static_cast<const uint8_t*>(d_ltabs8));
+      else
+        hipLaunchKernelGGL((hybrid_kernel<8, 4>), dim3(g), dim3(512), lds, s, a,
+                           static_cast<const uint8_t*>(d_ltabs8));
+    };
+    if (std::getenv("KB_HYBRID_FIRST")) vs.insert(vs.begin(), Variant{"hybrid 8+v", hv});
+    else vs.push_back(Variant{"hybrid 8+v", hv});
   }
   if (std::getenv("KB_PROD2"))  // the production dispatch again, at another place in the order
     vs.push_back(Variant{"prod dispatch (2nd)", [](const ApplyArgs& a, hipStream_t s) {
