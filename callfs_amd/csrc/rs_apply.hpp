@@ -202,6 +202,20 @@ __device__ __forceinline__ void mac_one(uint32_t (&acc)[U][RT][4], const uint4 (
 // kernel has registers to spare (R <= 4), 4 otherwise (8 took R = 8 from 68 to 73 VGPRs).
 template <int RT>
 constexpr int tail_loads() { return RT <= 4 ? 8 : 4; }
+// Which wave takes a stripe's ragged tail (S % 16 bytes): the block's last wave in the
+// stripe's last tile when that wave holds no vectors (the last tile is partial), so no
+// wave that streams vectors waits for the tail's byte loads; otherwise wave 0 of the
+// stripe's first tile. Returns the thread's byte index in the tail, or ~0u.
+// (tools/tail_probe.sh, profiles/r04/tail_probe/: odd S cost RS(20,4) 1.2, RS(12,4) 1.0,
+// RS(10,4) 0.5 points against S rounded down to 16 with the tail in the first tile.)
+template <int BS, int TV>
+__device__ __forceinline__ uint32_t tail_lane(uint64_t nvec, uint32_t tps, uint32_t tile) {
+  const uint64_t last = nvec - static_cast<uint64_t>(tps - 1) * TV;  // vectors in the last tile
+  if (last + 64 <= static_cast<uint64_t>(BS))  // the last wave of the last tile is idle
+    return tile == tps - 1 && threadIdx.x >= BS - 64 ? threadIdx.x - (BS - 64) : ~0u;
+  return tile == 0 ? threadIdx.x : ~0u;
+}
+
 template <int RT>
 __device__ __forceinline__ void tail_bytes(cptr<const uint8_t*> in, uint64_t b, int i0, int K,
                                            uint32_t (&x)[tail_loads<RT>()]) {
@@ -211,10 +225,10 @@ __device__ __forceinline__ void tail_bytes(cptr<const uint8_t*> in, uint64_t b, 
 template <int RT>
 __device__ __forceinline__ void vec_tail(const ApplyArgs& a, cptr<const uint8_t*> in,
                                          cptr<uint8_t*> out, uint32_t stripe,
-                                         cptr<uint32_t> tabs) {
+                                         cptr<uint32_t> tabs, uint32_t j) {
   const uint32_t nt = static_cast<uint32_t>(a.S - a.nvec * 16);
-  if (threadIdx.x >= nt) return;
-  const uint64_t b = a.nvec * 16 + threadIdx.x;
+  if (j >= nt) return;
+  const uint64_t b = a.nvec * 16 + j;
   uint32_t acc[RT];
 #pragma unroll
   for (int r = 0; r < RT; ++r) acc[r] = 0;
@@ -264,7 +278,10 @@ void rs_apply_vec(ApplyArgs a) {
     const uint64_t v0 = static_cast<uint64_t>(tile) * tile_vecs + threadIdx.x;
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * RT;
-    if (tile == 0 && a.tail_in_vec) vec_tail<RT>(a, in, out, stripe, tabs);
+    if (a.tail_in_vec) {
+      const uint32_t j = tail_lane<BS, BS * U>(a.nvec, tps, tile);
+      if (j != ~0u) vec_tail<RT>(a, in, out, stripe, tabs, j);
+    }
     bool live[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) live[u] = v0 + static_cast<uint64_t>(u) * BS < a.nvec;
@@ -669,11 +686,12 @@ __device__ __forceinline__ uint32_t lds_byte(const typename LdsAcc<RT>::T& t, in
 // at lds0 + 32*W*i + W*e / + 16*W + W*e.
 template <int RT>
 __device__ __forceinline__ void lds_tail(const ApplyArgs& a, cptr<const uint8_t*> in,
-                                         cptr<uint8_t*> out, uint32_t stripe, uint32_t lds0) {
+                                         cptr<uint8_t*> out, uint32_t stripe, uint32_t lds0,
+                                         uint32_t j) {
   constexpr int W = LdsAcc<RT>::W;
   const uint32_t nt = static_cast<uint32_t>(a.S - a.nvec * 16);
-  if (threadIdx.x >= nt) return;
-  const uint64_t b = a.nvec * 16 + threadIdx.x;
+  if (j >= nt) return;
+  const uint64_t b = a.nvec * 16 + j;
   typename LdsAcc<RT>::T t = lds_zero<RT>();
   for (int i0 = 0; i0 < a.K; i0 += tail_loads<RT>()) {
     uint32_t x[tail_loads<RT>()];
@@ -783,7 +801,10 @@ void rs_apply_lds(ApplyArgs a) {
     if constexpr (P::REALIGN == 2) {
       if (tile == 0) lds_edges<RT>(a, in, out, stripe, lds0);
     } else {
-      if (tile == 0 && a.tail_in_vec) lds_tail<RT>(a, in, out, stripe, lds0);
+      if (a.tail_in_vec) {
+        const uint32_t j = tail_lane<BS, TV>(a.nvec, tps, tile);
+        if (j != ~0u) lds_tail<RT>(a, in, out, stripe, lds0, j);
+      }
     }
     // lanes that store (REALIGN: lane 63 -- REALIGN 2: lanes 62, 63 -- and lanes past the
     // shard only load)

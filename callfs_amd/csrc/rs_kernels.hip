@@ -368,7 +368,6 @@ bool can_realign(const ApplyArgs& a) {
 bool can_wix(const ApplyArgs& a) {
   return a.R <= 4 && a.K >= 3 && a.K <= 96 && !(a.in_misalign | a.out_misalign);
 }
-bool has_verify_rows(const ApplyArgs& a) { return (a.verify_mask & ((1u << a.R) - 1)) != 0; }
 // CALLFS_RS_WIX=0 keeps every launch on the ring-of-three nibble kernel (A/B)
 bool wix_enabled() {
   static const bool on = [] {
@@ -392,13 +391,23 @@ bool wix_enabled() {
 // 71.9 -> 77.9, RS(8,8) 75.6 -> 77.6, RS(10,8) 74.4 -> 78.2, RS(4,2) read-only 82.8 ->
 // 88.0, RS(6,3) 1 MiB objects 71.4 -> 73.2, RS(10,4) 76.5 -> 75.9-76.1 (the tuner keeps
 // whichever is faster), RS(12,4) 77.2 -> 80.3 (G2).
-bool takes_tri(const ApplyArgs& a) {
+// The rule's triple-form order (tile_order.hpp tri_rule_order: round 4 adds X32 for K <= 4,
+// X32 / Q16 for K 5..6 and Q16 on 16-32 MiB power-of-two pitches), or -1. With
+// CALLFS_RS_TILE_ORDER set, the triple form follows the forced order with round 3's bounds.
+int tri_rule_of(const ApplyArgs& a) {
+  if (!wix_enabled() || !takes_lds(a)) return -1;
   const uint32_t rows = (1u << a.R) - 1;
   const uint64_t tps = (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;
-  return wix_enabled() && takes_lds(a) &&
-         tri_rule(a.K, a.R, (a.in_misalign | a.out_misalign) != 0, (a.verify_mask & rows) != 0,
-                  (a.verify_mask & rows) == rows, tps);
+  const bool mis = (a.in_misalign | a.out_misalign) != 0, verify = (a.verify_mask & rows) != 0,
+             read_only = (a.verify_mask & rows) == rows;
+  if (tile_order_override() >= 0)
+    return tri_rule(a.K, a.R, mis, verify, read_only, tps) &&
+                   (tps <= 256 || (tps <= 512 && a.K <= 6))
+               ? static_cast<int>(tri_order(lds_rule(a)))
+               : -1;
+  return tri_rule_order(a.K, a.R, mis, verify, read_only, tps, a.addr_tz, a.S, lds_rule(a));
 }
+bool takes_tri(const ApplyArgs& a) { return tri_rule_of(a) >= 0; }
 bool tri_tunable_launch(const ApplyArgs& a) {
   const uint32_t rows = (1u << a.R) - 1;
   return wix_enabled() && tri_tunable(a.K, a.R, (a.in_misalign | a.out_misalign) != 0,
@@ -474,7 +483,7 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
     const auto tri_in = [](TileOrder o) {
       return static_cast<TileOrder>(kOrderTri + static_cast<int>(o));
     };
-    if (takes_tri(a)) add(tri_in(tri_order(lds_rule(a))));  // the rule's kernel first
+    if (takes_tri(a)) add(tri_in(static_cast<TileOrder>(tri_rule_of(a))));  // the rule's kernel first
     add(lds_rule(a));
     if (can_realign(a)) {
       add(realign_in(TileOrder::kXcd32));
@@ -569,7 +578,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           }
           if (!tri && order < 0 && takes_tri(a)) tri = true;  // the rule: ord is the nibble rule's
           if (tri) {
-            const int ti = tri_index(order < 0 ? tri_order(ord) : ord);
+            const int ti = tri_index(order < 0 ? static_cast<TileOrder>(tri_rule_of(a)) : ord);
             fn = a.R <= 4 && (a.verify_mask & rows) && (a.verify_mask & rows) != rows
                      ? kLdsTriVerify[ti][a.R - 1]  // written + Verify rows: early compares
                      : kLdsTri[ti][a.R - 1];
@@ -706,7 +715,9 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
                        (order >= kOrderRealign || (order < 0 && takes_realign(a)));
   const TileOrder ord =
       realign    ? kRealignOrders[realign_order_index(order)]
-      : a.R <= 8 ? (order >= 0 ? static_cast<TileOrder>(order) : lds_rule(a))
+      : a.R <= 8 ? (order >= 0   ? static_cast<TileOrder>(order)
+                    : takes_tri(a) ? static_cast<TileOrder>(tri_rule_of(a))
+                                   : lds_rule(a))
                  : (order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a));
   const unsigned grid = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
   if (mode > 0) {  // the read streams alone / the write streams alone

@@ -129,25 +129,69 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
   return TileOrder::kConsecutive;
 }
 
+// The triple form's tile order for the order the nibble rule (or CALLFS_RS_TILE_ORDER)
+// picks: G8 (shards up to 256 KiB) and X8 -> X32, which ran within 0.6 points of G8 for the
+// 6-bit form at 1 MiB objects; every other order has its own triple instance.
+inline TileOrder tri_order(TileOrder nibble) {
+  switch (nibble) {
+    case TileOrder::kGroup8:
+    case TileOrder::kXcd8: return TileOrder::kXcd32;
+    default: return nibble;
+  }
+}
+
 // Triple-load form of an aligned R <= 8 LDS launch (Policy::WIX 2, rs_kernels.hip
 // takes_tri; DESIGN.md §5 "Shard triples"): the loads of three input shards issued
-// together, then their nibble lookups. Taken for 4 <= K <= 12 (shard sizes below) by
-// launches that write every row or compare every row; launches that mix written
-// and Verify rows keep the ring of three with its early compare loads (one-erasure decodes
-// ran 0.3-1.5 points slower in triples). RS(12,4) 77.2 -> 80.3 in G2; RS(16,4) gained 0.7
-// there and is left to rs_plan_tune.
-// Shard size bounds it. tools/profile_sweep.sh, the same box with the triple form
-// (profiles/r03/r03s5/profile_sweep.txt, taken up to 8 MiB shards) and without it above 2
-// MiB / at small S for K > 6 (profiles/r03/r03s6/profile_sweep.txt), % of 8 TB/s,
-// ring of three -> triples: RS(8,8) 8 MiB 71.7 -> 57.2, RS(8,4) 8 MiB 74.4 -> 67.1,
-// RS(12,4) 5.6 MB 74.8 -> 68.5, RS(10,4) 6.7 MB 74.2 -> 72.0, but RS(4,2) 4 MiB 69.6 ->
-// 78.4 and RS(6,3) 2.8 MB 72.4 -> 74.2; at small S RS(10,4) 105 KB 71.9 -> 68.5, RS(10,8)
-// 105 KB 65.2 -> 68.5, RS(4,2) 256 KiB 74.4 -> 78.2, RS(8,8) 128 KiB equal. So: S <= 2 MiB
-// (tps <= 256), or up to 4 MiB with K <= 6; at S <= 256 KiB only K <= 6 or R >= 5.
-inline bool tri_rule(int K, int R, bool misaligned, bool verify, bool read_only, uint64_t tps) {
-  if (R > 8 || K < 4 || K > 12 || misaligned || (verify && !read_only)) return false;
-  if (tps <= 32) return K <= 6 || R >= 5;
-  return tps <= 256 || (tps <= 512 && K <= 6);
+// together, then their nibble lookups. Returns the triple form's tile order (instances:
+// consecutive, G2, X32, Q8, Q16), or -1 for the ring of three in the nibble rule's order
+// `nibble`.
+//
+// Round 3 (tools/profile_sweep.sh, profiles/r03/r03s5 and r03s6): launches that write every
+// row or compare every row, shards up to 2 MiB, up to 4 MiB with K <= 6, and at <= 256 KiB
+// only K <= 6 or R >= 5, in the nibble rule's order (G8 -> X32): RS(4,2) 1 MiB 72 -> 80.6,
+// RS(10,8) 74.4 -> 78.2, RS(12,4) 77.2 -> 80.3.
+// Round 4 (tools/tri_sweep.sh, profiles/r04/tri_sweep1 and tri_sweep2, two runs; shapes
+// outside the fit in profiles/r04/tri_validate; % of 8 TB/s, round-3 rule -> this rule):
+//  * write every row, K <= 5: X32 at every size above 256 KiB: RS(4,2) 1 MiB 79.2 -> 81.0,
+//    2 MiB 81.0 -> 84.1, 4 MiB 77.9 -> 80.2, 8 MiB 70.0 -> 79.6, 16 MiB 69.9 -> 72.9,
+//    32 MiB 69.8 -> 78.0, 64 MiB 72.2 -> 82.2; RS(5,3) 8 MiB 73.7 -> 77.9, 16 MiB -> 75.7;
+//  * write every row, K = 6: X32 up to 2 MiB, Q16 above: RS(6,3) 1 MiB 74.6 -> 75.3,
+//    2.8 MB 74.1 -> 77.6, 4 MiB 71.7 -> 77.3, 8 MiB 73.2 -> 74.5, 11.2 MB 73.3 -> 75.2,
+//    16 MiB 73.2 -> 76.5, 32 MiB 74.4 -> 76.4; RS(6,6) 16 MiB 72.6 -> 74.0;
+//  * write every row, K = 7..12 on power-of-two pitches of 16-32 MiB (addr_tz >= 24): Q16:
+//    RS(8,4) 16 MiB 74.1 -> 77.7, RS(10,4) 74.0 -> 77.5, RS(12,4) 71.8 -> 77.4, RS(9,3)
+//    76.0 -> 77.5; elsewhere round 3's rule;
+//  * compare every row (the download's Verify with nothing lost): X32 at every size above
+//    256 KiB: RS(4,2) 8 MiB 82.7 -> 90.5, RS(6,3) 16 MiB 85.7 -> 90.0, RS(8,4) 8 MiB 85.7 ->
+//    88.1, RS(10,4) 4 MiB 84.9 -> 86.3, 16 MiB 84.4 -> 87.8;
+//  * R <= 4 with written and Verify rows (the one-erasure decode), the kernel with early
+//    compare loads (Policy::VPF): K <= 4 in X32 (RS(4,2) 1 MiB erase {1} 76.2 -> 80.1,
+//    4 MiB {0} 76.7 -> 81.1), K 5..12 up to 1 MiB in the nibble rule's order (G2: RS(6,3)
+//    {2} 74.2 -> 75.0, RS(8,4) {5} 77.5 -> 78.3, RS(12,4) {7} 74.4 -> 75.7, RS(10,4) {5}
+//    / {13} / {0} +0.2 / +0.1 / -0.8); larger shards keep the ring (RS(10,4) 6.7 MB {5}
+//    76.3 -> 74.5 in triples).
+inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_only,
+                          uint64_t tps, int addr_tz, uint64_t S, TileOrder nibble) {
+  if (R > 8 || K < 4 || K > 12 || misaligned) return -1;
+  const int x32 = static_cast<int>(TileOrder::kXcd32), q16 = static_cast<int>(TileOrder::kSeg16);
+  if (verify && !read_only) {  // written + Verify rows: only the R <= 4 early-compare form
+    if (R > 4) return -1;
+    if (K <= 4) return x32;
+    if (tps <= 32) return K <= 6 ? x32 : -1;  // as for written rows at small S
+    return tps <= 128 ? static_cast<int>(tri_order(nibble)) : -1;
+  }
+  if (tps <= 32) return K <= 6 || R >= 5 ? x32 : -1;
+  if (read_only) return x32;
+  if (K <= 5) return x32;
+  if (K == 6) return tps <= 256 ? x32 : q16;
+  if (addr_tz >= 24 && S >= (16ull << 20) && S <= (32ull << 20)) return q16;
+  if (tps <= 256) return static_cast<int>(tri_order(nibble));
+  return -1;
+}
+inline bool tri_rule(int K, int R, bool misaligned, bool verify, bool read_only, uint64_t tps,
+                     int addr_tz = 0, uint64_t S = 0) {
+  return tri_rule_order(K, R, misaligned, verify, read_only, tps, addr_tz, S,
+                        TileOrder::kConsecutive) >= 0;
 }
 // Triple loads in the realigning kernel (misaligned shards, upstream Split layout):
 // measured in round 4 (DESIGN.md §5 "Shard triples"); until then only rs_plan_tune and
@@ -161,17 +205,6 @@ inline bool realign_tri_rule(int K, int R, bool verify, bool read_only) {
 // compare loads, Policy::VPF)
 inline bool tri_tunable(int K, int R, bool misaligned, bool verify, bool read_only) {
   return R <= 8 && K >= 3 && K <= 16 && !misaligned && (!verify || read_only || R <= 4);
-}
-// The triple form's tile order (instances: consecutive, G2, X32) for the order the nibble
-// rule picks: G8 (shards up to 256 KiB) -> X32, which ran within 0.6 points of G8 for the
-// 6-bit form at 1 MiB objects.
-inline TileOrder tri_order(TileOrder nibble) {
-  switch (nibble) {
-    case TileOrder::kGroup2: return TileOrder::kGroup2;
-    case TileOrder::kGroup8:
-    case TileOrder::kXcd32: return TileOrder::kXcd32;
-    default: return TileOrder::kConsecutive;
-  }
 }
 // Wide groups hold 19-32 shard streams per stripe; from 2 MiB shards on, 8 interleaved
 // column segments beat consecutive tiles (tools/order_sweep.sh, KB_ORD, 9 rounds, % of

@@ -287,9 +287,17 @@ int main() {
     CHECK(vec_tile_order(349526, tps_of(349526), 8) == TileOrder::kGroup2);
     CHECK(vec_tile_order(16 * MiB, tps_of(16 * MiB), 24) == TileOrder::kSeg16);
     CHECK(vec_tile_order(107374183, tps_of(107374183), 8) == TileOrder::kConsecutive);
-    // triple loads: aligned R <= 8 launches with 4..10 inputs that write every row or
-    // compare every row, shards up to 8 MiB
+    // triple loads (tri_rule_order): aligned R <= 8 launches with 4..12 inputs that write
+    // every row or compare every row; round 3's bounds (shards up to 2 MiB, 4 MiB with
+    // K <= 6) in the nibble rule's order, and since round 4 K <= 4 at any size in X32, K 5..6
+    // in X32 / Q16, K 7..12 on 16-32 MiB power-of-two pitches in Q16
     const uint64_t t1 = tps_of(MiB);
+    const int X32 = static_cast<int>(TileOrder::kXcd32), Q16 = static_cast<int>(TileOrder::kSeg16),
+              G2 = static_cast<int>(TileOrder::kGroup2);
+    auto tro = [](int K, int R, uint64_t S, int tz, bool verify = false, bool ro = false,
+                  TileOrder nib = TileOrder::kGroup2) {
+      return tri_rule_order(K, R, false, verify, ro, (S / 16 + 511) / 512, tz, S, nib);
+    };
     CHECK(tri_rule(4, 2, false, false, false, t1));   // CallFS default RS(4,2) encode
     CHECK(tri_rule(10, 4, false, false, false, t1));  // the bench shape
     CHECK(tri_rule(8, 8, false, false, false, t1));   // 8-byte entries too
@@ -298,21 +306,36 @@ int main() {
     CHECK(tri_rule(12, 4, false, false, false, t1));
     CHECK(!tri_rule(16, 4, false, false, false, t1)); // the tuner decides
     CHECK(!tri_rule(4, 2, true, false, false, t1));   // Split layout: realigning kernel
-    CHECK(!tri_rule(6, 3, false, true, false, t1));   // written + Verify rows: early compares
+    CHECK(tri_rule(6, 3, false, true, false, t1));    // written + Verify rows: early compares
+    CHECK(!tri_rule(6, 6, false, true, false, t1));   // ... at R <= 4 only
     CHECK(!tri_rule(10, 9, false, false, false, t1)); // 16-byte entries
-    CHECK(!tri_rule(4, 2, false, false, false, tps_of(16 * MiB)));
     CHECK(!tri_rule(8, 8, false, false, false, tps_of(8 * MiB)));     // 8 MiB shards: lost
     CHECK(tri_rule(8, 4, false, false, false, tps_of(2 * MiB)));      // 2 MiB: gained
     CHECK(tri_rule(4, 2, false, false, false, tps_of(256 << 10)));    // small S, few inputs
     CHECK(!tri_rule(10, 4, false, false, false, tps_of(104858)));     // small S, 10 inputs
     CHECK(tri_rule(10, 8, false, false, false, tps_of(104858)));      // small S, R = 8
-    CHECK(tri_rule(4, 2, false, false, false, tps_of(4 * MiB)));      // 4 MiB, few inputs
     CHECK(!tri_rule(10, 4, false, false, false, tps_of(4 * MiB)));
     CHECK(!tri_rule(10, 4, false, false, false, tps_of(6710887)));    // configs[2] shards
+    // round 4: K <= 4 in X32 at every size (RS(4,2) 8 MiB 70.0 -> 79.6, 32 MiB 69.8 -> 78.0)
+    CHECK(tro(4, 2, MiB, 20) == X32 && tro(4, 2, 16 * MiB, 24) == X32 && tro(4, 2, 64 * MiB, 26) == X32);
+    CHECK(tro(4, 2, 5592406, 8) == X32);
+    // K 5..6: X32 up to 2 MiB, Q16 above (RS(6,3) 4 MiB 71.7 -> 77.3, 16 MiB 73.2 -> 76.5)
+    CHECK(tro(6, 3, MiB, 20) == X32 && tro(6, 3, 2796203, 8) == Q16 && tro(6, 3, 16 * MiB, 24) == Q16);
+    // K 7..12: Q16 on 16-32 MiB power-of-two pitches, round 3's rule elsewhere
+    CHECK(tro(10, 4, 16 * MiB, 24) == Q16 && tro(12, 4, 32 * MiB, 25) == Q16);
+    CHECK(tro(10, 4, 16 * MiB, 8) == -1 && tro(10, 4, 64 * MiB, 26) == -1);
+    CHECK(tro(10, 4, MiB, 20) == G2);  // the nibble rule's order (G2 for the bench shape)
+    // read-only launches: X32 at every size above 256 KiB (RS(6,3) 16 MiB 85.7 -> 90.0)
+    CHECK(tro(4, 2, 16 * MiB, 24, true, true) == X32 && tro(10, 4, MiB, 20, true, true, TileOrder::kXcd32) == X32);
+    // written + Verify rows (R <= 4, early compares): K <= 4 in X32, K 5..12 up to 1 MiB
+    CHECK(tro(4, 2, MiB, 20, true, false) == X32 && tro(4, 2, 4 * MiB, 22, true, false) == X32);
+    CHECK(tro(10, 4, MiB, 20, true, false) == G2 && tro(10, 4, 6710887, 8, true, false) == -1);
+    CHECK(tro(10, 4, 104858, 8, true, false) == -1 && tro(6, 3, 174763, 8, true, false) == X32);
     CHECK(tri_tunable(16, 4, false, false, false) && !tri_tunable(20, 4, false, false, false));
     CHECK(tri_order(TileOrder::kGroup8) == TileOrder::kXcd32);
     CHECK(tri_order(TileOrder::kGroup2) == TileOrder::kGroup2);
     CHECK(tri_order(TileOrder::kConsecutive) == TileOrder::kConsecutive);
+    CHECK(tri_order(TileOrder::kSeg16) == TileOrder::kSeg16 && tri_order(TileOrder::kXcd8) == TileOrder::kXcd32);
   }
   // 6. multi-device placement (dispatch.hpp), mocked device counts
   {

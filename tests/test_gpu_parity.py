@@ -1346,13 +1346,19 @@ def test_plan_wix_triples_vs_oracle(native_lib, k, m, S, order):
     (10, 4, 1 << 20, (0, 1, 2, 3)),      # the bench decode
     (4, 2, 1 << 20, ()),                 # download Verify, nothing erased: read-only
     (10, 4, 100_000 + 3, ()),            # read-only, ragged tail compared too
-    (5, 3, 1 << 18, (1,)),               # written + Verify rows: ring of three (no triples)
+    (5, 3, 1 << 18, (1,)),               # written + Verify rows: triples with early compares (G2)
+    (4, 2, (8 << 20) + 16, None),        # K <= 5 above 2 MiB: X32 (round 4)
+    (6, 3, (4 << 20) + 32, None),        # K = 6 above 2 MiB: Q16
+    (4, 2, (4 << 20) + 7, (1,)),         # K <= 4, written + Verify rows: X32, early compares
+    (10, 4, 1 << 20, (5,)),              # one-erasure decode of the bench shape: G2
+    (6, 3, (16 << 20) + 48, ()),         # read-only above 2 MiB: X32
 ])
 def test_plan_rule_triples_vs_oracle(native_lib, k, m, S, erase):
-    """The rule's triple-load kernel (4 <= K <= 10, R <= 8, launches that write every row
-    or compare every row): encode / reconstruct every byte of every stripe as the oracle
-    does; read-only launches pass clean stripes and flag exactly the stripe with a flipped
-    byte, also in the ragged tail."""
+    """The rule's triple-load kernel (tile_order.hpp tri_rule_order: 4 <= K <= 12, R <= 8;
+    launches that write every row or compare every row, and R <= 4 launches with written
+    and Verify rows through the early-compare form): encode / reconstruct every byte of
+    every stripe as the oracle does; launches with Verify rows pass clean stripes and flag
+    exactly the stripe with a flipped byte, also in the ragged tail."""
     import torch
     from callfs_amd.device import Plan
     n, batch = k + m, 3

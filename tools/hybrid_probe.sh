@@ -8,6 +8,7 @@ cd /tmp && export TMPDIR=/tmp
 PA="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
 PB="GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
 for sh in "32 16" "20 16" "10 16" "10 12"; do
+  unset KB_HYBRID KB_HYBRID_FIRST
   set -- $sh; k=$1; m=$2; B=$(( k >= 20 ? 128 : 256 ))
   KB_HYBRID=1 KB_KEEP="hybrid" timeout -k 10 150 "$R/tools/kbench" $k $m 1048576 $B 5 10 > "$OUT/time_${k}_${m}.log" 2>&1 || exit $?
   grep -E "prod dispatch|hybrid|MISMATCH" "$OUT/time_${k}_${m}.log" | sed "s/^/RS($k,$m) /"
