@@ -154,13 +154,13 @@ inline TileOrder tri_order(TileOrder nibble) {
 // outside the fit in profiles/r04/tri_validate; % of 8 TB/s, round-3 rule -> this rule):
 //  * write every row, K <= 5: X32 at every size above 256 KiB: RS(4,2) 1 MiB 79.2 -> 81.0,
 //    2 MiB 81.0 -> 84.1, 4 MiB 77.9 -> 80.2, 8 MiB 70.0 -> 79.6, 16 MiB 69.9 -> 72.9,
-//    32 MiB 69.8 -> 78.0, 64 MiB 72.2 -> 82.2; RS(5,3) 8 MiB 73.7 -> 77.9, 16 MiB -> 75.7;
+//    32 MiB 69.8 -> 78.0, 64 MiB 71.5 -> 82.2; RS(5,3) 8 MiB 71.2 -> 77.9, 16 MiB 70.4 -> 75.7;
 //  * write every row, K = 6: X32 up to 2 MiB, Q16 above: RS(6,3) 1 MiB 74.6 -> 75.3,
 //    2.8 MB 74.1 -> 77.6, 4 MiB 71.7 -> 77.3, 8 MiB 73.2 -> 74.5, 11.2 MB 73.3 -> 75.2,
-//    16 MiB 73.2 -> 76.5, 32 MiB 74.4 -> 76.4; RS(6,6) 16 MiB 72.6 -> 74.0;
+//    16 MiB 73.2 -> 76.5, 32 MiB 73.8 -> 76.4; RS(6,6) 16 MiB 73.0 -> 74.0;
 //  * write every row, K = 7..12 on power-of-two pitches of 16-32 MiB (addr_tz >= 24): Q16:
 //    RS(8,4) 16 MiB 74.1 -> 77.7, RS(10,4) 74.0 -> 77.5, RS(12,4) 71.8 -> 77.4, RS(9,3)
-//    76.0 -> 77.5; elsewhere round 3's rule;
+//    74.6 -> 77.5; elsewhere round 3's rule;
 //  * compare every row (the download's Verify with nothing lost): X32 at every size above
 //    256 KiB: RS(4,2) 8 MiB 82.7 -> 90.5, RS(6,3) 16 MiB 85.7 -> 90.0, RS(8,4) 8 MiB 85.7 ->
 //    88.1, RS(10,4) 4 MiB 84.9 -> 86.3, 16 MiB 84.4 -> 87.8;

@@ -434,6 +434,23 @@ int main(int argc, char** argv) {
       case 4: KB_VORD(4) break;
     }
   }
+  if (m <= 4 && std::getenv("KB_TRIORD")) {  // triple loads (WIX 2) in every tile order
+#define KB_TP(ORD) Policy<8, 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, 2>
+#define KB_TRI(RT, ORD, NAME) \
+  vs.push_back(Variant{NAME, [](const ApplyArgs& a, hipStream_t s) { launch_lds<RT, KB_TP(ORD)>(a, s); }});
+#define KB_TRIS(RT) KB_TRI(RT, 0, "tri ord consec") KB_TRI(RT, 2, "tri ord g8") KB_TRI(RT, 4, "tri ord g4") \
+  KB_TRI(RT, 5, "tri ord g2") KB_TRI(RT, 6, "tri ord q8") KB_TRI(RT, 7, "tri ord q32") KB_TRI(RT, 8, "tri ord q16") \
+  KB_TRI(RT, 9, "tri ord q64") KB_TRI(RT, 10, "tri ord x8") KB_TRI(RT, 11, "tri ord x32")
+    switch (m) {
+      case 1: KB_TRIS(1) break;
+      case 2: KB_TRIS(2) break;
+      case 3: KB_TRIS(3) break;
+      case 4: KB_TRIS(4) break;
+    }
+#undef KB_TRIS
+#undef KB_TRI
+#undef KB_TP
+  }
   if ((m == 2 || m == 3 || m == 4 || m == 8) && std::getenv("KB_ORD")) {  // LDS kernel tile orders
     using O0 = Policy<2, 1, true, true, false, 512, 2, 0>;
     using O2 = Policy<2, 1, true, true, false, 512, 2, 2>;
