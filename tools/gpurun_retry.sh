@@ -1,13 +1,13 @@
 # Runs one gpurun call; repeats it only while gpurun reports an infrastructure event
-# (status "transient" or exit 3: no box, nothing charged, nothing ran), at most 6 times.
+# (status "transient" or exit 3: no box, nothing charged, nothing ran), at most 10 times.
 # A command that ran and failed is never repeated.
 # Usage: bash tools/gpurun_retry.sh <timeout_s> <log> '<command>'
 t=$1; log=$2; cmd=$3
-for i in 1 2 3 4 5 6; do
+for i in 1 2 3 4 5 6 7 8 9 10; do
   /usr/local/graft/bin/gpurun --timeout "$t" -- "$cmd" > "$log" 2>&1; rc=$?
   st=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json')).get('status',''))" 2>/dev/null)
   if [ "$rc" = 3 ] || { [ "$st" = transient ] && grep -q "retry" "$log"; }; then
-    echo "attempt $i: infrastructure ($rc/$st), retrying in 60 s" >> "$log.retries"; sleep 60; continue
+    echo "attempt $i: infrastructure ($rc/$st), retrying in 90 s" >> "$log.retries"; sleep 90; continue
   fi
   exit $rc
 done

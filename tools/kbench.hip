@@ -642,6 +642,36 @@ int main(int argc, char** argv) {
                          CK(hipMemcpyAsync(buf + half, buf, half, hipMemcpyDeviceToDevice, s));
                        }, false});
 
+  if (std::getenv("KB_PERSIST") && m <= 8) {  // persistent grids of N blocks per CU (small-S probe)
+    // the production LDS policy (G8 order, ring of three) with PERSIST: a fixed grid of
+    // 256 * N blocks strides over the tiles, so N bounds the tiles (and stripes) in flight
+#define KB_PP Policy<2, 1, true, true, true, 512, 2, 2>
+#define KB_PV(R) [](const ApplyArgs& a, hipStream_t s, unsigned g) { \
+    hipLaunchKernelGGL((dev::rs_apply_lds<R, KB_PP>), dim3(g), dim3(512), dev::lds_bytes(a.K, R), s, a); }
+    static void (*const pl[8])(const ApplyArgs&, hipStream_t, unsigned) = {
+        KB_PV(1), KB_PV(2), KB_PV(3), KB_PV(4), KB_PV(5), KB_PV(6), KB_PV(7), KB_PV(8)};
+#undef KB_PV
+    static const int mm = m;
+    for (int nb : {1, 2, 3, 4}) {
+      static std::string names[5];
+      names[nb] = "persist " + std::to_string(nb);
+      vs.push_back(Variant{names[nb], [nb](const ApplyArgs& a, hipStream_t s) {
+                             pl[mm - 1](a, s, dev::vec_grid<KB_PP>(a.nvec, a.batch, nb));
+                           }});
+    }
+#undef KB_PP
+  }
+  // KB_ONLY=name: time only the variant of exactly that name (PMC passes of one variant)
+  if (const char* only = std::getenv("KB_ONLY")) {
+    std::vector<Variant> one;
+    for (auto& v : vs)
+      if (v.name == only) one.push_back(v);
+    if (one.empty()) {
+      std::fprintf(stderr, "KB_ONLY: no variant named %s\n", only);
+      return 2;
+    }
+    vs.swap(one);
+  }
   // KB_KEEP="a|b|...": keep only the variants whose name contains one of these (the
   // first variant, the production dispatch, is always kept: it is the parity reference)
   if (const char* keep = std::getenv("KB_KEEP")) {
