@@ -498,10 +498,11 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
     add(TileOrder::kConsecutive);
     add(TileOrder::kGroup2);
     if (tps <= 32) add(TileOrder::kGroup8);
-    if (tps > 1024 || (every_instance && tps >= 64)) {
-      add(TileOrder::kSeg8);
-      add(TileOrder::kSeg16);
-    }
+    // Q8 from 64 tiles per stripe (8 segments of >= 8 tiles): at 1 MiB shards it ran within
+    // a point of the best order and ahead of the rule's on some boxes (RS(16,4) 77.7 vs 76.8,
+    // profiles/r04/tri_sweep1); Q16 above 8 MiB as before
+    if (tps >= 64) add(TileOrder::kSeg8);
+    if (tps > 1024 || (every_instance && tps >= 64)) add(TileOrder::kSeg16);
     if (every_instance) {  // on aligned shards never faster than the rule's order, which
                            // is X32 itself for read-only launches
       add(TileOrder::kXcd8);
@@ -511,10 +512,10 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(tri_in(TileOrder::kConsecutive));
       add(tri_in(TileOrder::kGroup2));
       add(tri_in(TileOrder::kXcd32));
-      if (tps > 1024 || (every_instance && tps >= 64)) {
-        add(tri_in(TileOrder::kSeg8));
-        add(tri_in(TileOrder::kSeg16));
-      }
+      // tri-Q8 from 64 tiles per stripe (RS(10,4) 1 MiB 77.5 / 77.3 against 76.3 / 76.2 for
+      // tri-G2, profiles/r04/tri_sweep1, tri_sweep2); tri-Q16 above 8 MiB
+      if (tps >= 64) add(tri_in(TileOrder::kSeg8));
+      if (tps > 1024 || (every_instance && tps >= 64)) add(tri_in(TileOrder::kSeg16));
     }
     if (every_instance && can_wix(a)) {  // WIX: A/B instances only
       const int n0 = static_cast<int>(c.size());

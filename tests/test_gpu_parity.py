@@ -1593,3 +1593,42 @@ def test_small_path_every_byte_right_after_flag(native_lib, k, m, S, B):
             want = cref.encode(stripes[b], k, m)
             for j in range(m):
                 assert bytes(parity[b][j]) == bytes(want[j]), (rep, b, j)
+
+
+@pytest.mark.parametrize("k,m,S", [
+    (10, 4, 16 * 512 * 3 + 5),          # last tile full: the tail in tile 0's wave 0
+    (10, 4, 16 * (512 * 3 + 100) + 7),  # last tile partial: its idle last wave takes the tail
+    (10, 4, 16 * (512 * 2 + 448) + 9),  # 448 vectors: the last wave exactly idle
+    (10, 4, 16 * (512 * 2 + 449) + 3),  # 449: the last wave holds one vector -> tile 0
+    (10, 4, 16 * 40 + 11),              # one partial tile: first and last tile coincide
+    (3, 2, 16 * (512 + 77) + 13),       # v_perm kernel (k <= 3), partial last tile
+    (3, 2, 16 * 1024 + 1),              # v_perm kernel, full last tile
+    (12, 8, 16 * (512 * 4 + 300) + 15),  # R = 8, triple loads at this size
+    (20, 16, 16 * (512 + 10) + 2),       # wide group (16-byte entries)
+])
+def test_ragged_tail_wave_placement(native_lib, k, m, S):
+    """The S % 16 tail bytes of every stripe go to the idle last wave of the stripe's last
+    tile when that tile is partial, else to wave 0 of its first tile (rs_apply.hpp
+    tail_lane): encode every byte against the oracle, and a decode with Verify rows flags
+    a flipped last byte (which only the tail wave computes) in exactly its stripe."""
+    import torch
+    from callfs_amd.device import Plan
+    batch = 3
+    sb = _batch(k, m, S, batch, seed=S)
+    Plan.for_batch(sb).launch()
+    torch.cuda.synchronize()
+    h = sb.buf[:, :, :S].cpu().numpy()
+    for b in range(batch):
+        want = cref.encode([h[b, i] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(h[b, k + j], want[j]), (b, j)
+    n = k + m
+    present = [i != 0 for i in range(n)]  # one erasure: m - 1 Verify rows
+    dec = Plan.for_batch(sb, present=present)
+    sb.buf[:, 0].zero_()
+    dec.launch()
+    assert not dec.corrupt()
+    assert np.array_equal(sb.buf[:, :, :S].cpu().numpy(), h)
+    sb.buf[1, n - 1, S - 1] ^= 0x20
+    dec.launch()
+    assert dec.corrupt_stripes() == [1]
