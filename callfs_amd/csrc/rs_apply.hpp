@@ -861,19 +861,96 @@ void rs_apply_lds(ApplyArgs a) {
           x1 = x2;
         }
       }
+    } else if constexpr (P::WIX == 3) {
+      // triples double-buffered in two register sets, with no conditional load anywhere:
+      // the loop runs while both its triples exist, and the last one or two triples with
+      // the K % 3 remainder run as straight-line tails, one per case (a load skipped on a
+      // runtime condition, or a join after one, makes the compiler wait for every load in
+      // flight). Set A is consumed while set B loads and vice versa. K >= 3.
+      const int KT = K / 3, rem = K - 3 * KT;
+      const uint32_t tb = 32u * W;
+      auto mac3 = [&](const uint4& y0, const uint4& y1, const uint4& y2, int g) {
+        const uint32_t b = lds0 + static_cast<uint32_t>(3 * g) * tb;
+        lds_mac<RT>(acc, y0, b);
+        lds_mac<RT>(acc, y1, b + tb);
+        lds_mac<RT>(acc, y2, b + 2 * tb);
+      };
+      auto mac_rem = [&](const uint4& y0, const uint4& y1, int n) {
+        const uint32_t b = lds0 + static_cast<uint32_t>(3 * KT) * tb;
+        if (n > 0) lds_mac<RT>(acc, y0, b);
+        if (n > 1) lds_mac<RT>(acc, y1, b + tb);
+      };
+      uint4 a0 = ld(0), a1 = ld(1), a2 = ld(2), b0, b1, b2;
+      int g = 0;
+#pragma unroll 1
+      for (; g + 2 < KT; g += 2) {
+        b0 = ld(3 * g + 3);
+        b1 = ld(3 * g + 4);
+        b2 = ld(3 * g + 5);
+        __builtin_amdgcn_sched_barrier(0);  // the loads stay ahead of the lookups
+        mac3(a0, a1, a2, g);
+        a0 = ld(3 * g + 6);
+        a1 = ld(3 * g + 7);
+        a2 = ld(3 * g + 8);
+        __builtin_amdgcn_sched_barrier(0);
+        mac3(b0, b1, b2, g + 1);
+      }
+      const int i = 3 * g + 3;  // first shard after triple g
+      if (KT - g == 2) {        // triples g (in A) and g + 1, then the remainder
+        b0 = ld(i);
+        b1 = ld(i + 1);
+        b2 = ld(i + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        if (rem == 0) {
+          mac3(a0, a1, a2, g);
+          mac3(b0, b1, b2, g + 1);
+        } else if (rem == 1) {
+          mac3(a0, a1, a2, g);
+          a0 = ld(i + 3);
+          __builtin_amdgcn_sched_barrier(0);
+          mac3(b0, b1, b2, g + 1);
+          mac_rem(a0, a0, 1);
+        } else {
+          mac3(a0, a1, a2, g);
+          a0 = ld(i + 3);
+          a1 = ld(i + 4);
+          __builtin_amdgcn_sched_barrier(0);
+          mac3(b0, b1, b2, g + 1);
+          mac_rem(a0, a1, 2);
+        }
+      } else {  // triple g (in A), then the remainder
+        if (rem == 0) {
+          mac3(a0, a1, a2, g);
+        } else if (rem == 1) {
+          b0 = ld(i);
+          __builtin_amdgcn_sched_barrier(0);
+          mac3(a0, a1, a2, g);
+          mac_rem(b0, b0, 1);
+        } else {
+          b0 = ld(i);
+          b1 = ld(i + 1);
+          __builtin_amdgcn_sched_barrier(0);
+          mac3(a0, a1, a2, g);
+          mac_rem(b0, b1, 2);
+        }
+      }
     } else if constexpr (P::WIX) {
       // triples: the next triple's three loads are in flight while one is consumed; the
-      // K % 3 shards left over take the nibble tables
+      // K % 3 shards left over take the nibble tables (WIX 4, A/B probe: loads past K
+      // leave zeros instead of a copy of x0)
       const int KT = K / 3;
       // VPF: the Verify rows' compare loads go out with the triple whose loads reach K - VPF
       // (or with the last triple when the remainder shards do)
       const int gv = kVpf ? std::min(KT - 1, (std::max(3, K - P::VPF) - 3) / 3) : -1;
-      uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : x0, x2 = K > 2 ? ld(2) : x0;
+      constexpr bool kz = P::WIX == 4;
+      const uint4 zv = make_uint4(0, 0, 0, 0);
+      uint4 x0 = ld(0), x1 = K > 1 ? ld(1) : (kz ? zv : x0), x2 = K > 2 ? ld(2) : (kz ? zv : x0);
 #pragma unroll 1
       for (int g = 0; g < KT; ++g) {
         const int i = 3 * g + 3;
-        const uint4 n0 = i < K ? ld(i) : x0, n1 = i + 1 < K ? ld(i + 1) : x0,
-                    n2 = i + 2 < K ? ld(i + 2) : x0;
+        const uint4 d = kz ? zv : x0;
+        const uint4 n0 = i < K ? ld(i) : d, n1 = i + 1 < K ? ld(i + 1) : d,
+                    n2 = i + 2 < K ? ld(i + 2) : d;
         if constexpr (kVpf) {
           if (g == gv) {
 #pragma unroll

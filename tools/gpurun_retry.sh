@@ -7,7 +7,8 @@ for i in 1 2 3 4 5 6 7 8 9 10; do
   /usr/local/graft/bin/gpurun --timeout "$t" -- "$cmd" > "$log" 2>&1; rc=$?
   st=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json')).get('status',''))" 2>/dev/null)
   if [ "$rc" = 3 ] || { [ "$st" = transient ] && grep -q "retry" "$log"; }; then
-    echo "attempt $i: infrastructure ($rc/$st), retrying in 90 s" >> "$log.retries"; sleep 90; continue
+    w=$(grep -o "retry in [0-9]*s" "$log" | tail -1 | tr -dc 0-9); w=${w:-90}; [ "$w" -lt 90 ] && w=90
+    echo "attempt $i: infrastructure ($rc/$st), retrying in $w s" >> "$log.retries"; sleep "$w"; continue
   fi
   exit $rc
 done
