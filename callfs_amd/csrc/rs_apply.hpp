@@ -861,77 +861,74 @@ void rs_apply_lds(ApplyArgs a) {
           x1 = x2;
         }
       }
-    } else if constexpr (P::WIX == 3) {
-      // triples double-buffered in two register sets, with no conditional load anywhere:
-      // the loop runs while both its triples exist, and the last one or two triples with
-      // the K % 3 remainder run as straight-line tails, one per case (a load skipped on a
-      // runtime condition, or a join after one, makes the compiler wait for every load in
-      // flight). Set A is consumed while set B loads and vice versa. K >= 3.
-      const int KT = K / 3, rem = K - 3 * KT;
+    } else if constexpr (P::WIX == 3 || P::WIX == 5) {
+      // groups of G = 3 (WIX 3) or 2 (WIX 5) shards double-buffered in two register sets,
+      // with no conditional load anywhere: the loop runs while both its groups exist, and
+      // the last one or two groups with the K % G remainder run as straight-line tails, one
+      // per case (a load skipped on a runtime condition, or a join after one, makes the
+      // compiler wait for every load in flight; so do the rotation copies of a ring). Set A
+      // is consumed while set B loads and vice versa: 2G loads in flight. K >= G.
+      constexpr int G = P::WIX == 3 ? 3 : 2;
+      const int KG = K / G, rem = K - G * KG;
       const uint32_t tb = 32u * W;
-      auto mac3 = [&](const uint4& y0, const uint4& y1, const uint4& y2, int g) {
-        const uint32_t b = lds0 + static_cast<uint32_t>(3 * g) * tb;
-        lds_mac<RT>(acc, y0, b);
-        lds_mac<RT>(acc, y1, b + tb);
-        lds_mac<RT>(acc, y2, b + 2 * tb);
+      uint4 A[G], B[G];
+      auto load_g = [&](uint4 (&x)[G], int i0) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) x[j] = ld(i0 + j);
+        __builtin_amdgcn_sched_barrier(0);  // the loads stay ahead of the lookups
       };
-      auto mac_rem = [&](const uint4& y0, const uint4& y1, int n) {
-        const uint32_t b = lds0 + static_cast<uint32_t>(3 * KT) * tb;
-        if (n > 0) lds_mac<RT>(acc, y0, b);
-        if (n > 1) lds_mac<RT>(acc, y1, b + tb);
+      auto mac_g = [&](const uint4 (&x)[G], int i0, int n) {
+        const uint32_t b = lds0 + static_cast<uint32_t>(i0) * tb;
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+          if (j < n) lds_mac<RT>(acc, x[j], b + static_cast<uint32_t>(j) * tb);
       };
-      uint4 a0 = ld(0), a1 = ld(1), a2 = ld(2), b0, b1, b2;
+      auto load_rem = [&](uint4 (&x)[G], int i0, int n) {  // n = 1 .. G - 1, uniform
+        if (n == 1) {
+          x[0] = ld(i0);
+        } else {
+          x[0] = ld(i0);
+          x[1] = ld(i0 + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      load_g(A, 0);
       int g = 0;
 #pragma unroll 1
-      for (; g + 2 < KT; g += 2) {
-        b0 = ld(3 * g + 3);
-        b1 = ld(3 * g + 4);
-        b2 = ld(3 * g + 5);
-        __builtin_amdgcn_sched_barrier(0);  // the loads stay ahead of the lookups
-        mac3(a0, a1, a2, g);
-        a0 = ld(3 * g + 6);
-        a1 = ld(3 * g + 7);
-        a2 = ld(3 * g + 8);
-        __builtin_amdgcn_sched_barrier(0);
-        mac3(b0, b1, b2, g + 1);
+      for (; g + 2 < KG; g += 2) {
+        load_g(B, G * g + G);
+        mac_g(A, G * g, G);
+        load_g(A, G * g + 2 * G);
+        mac_g(B, G * g + G, G);
       }
-      const int i = 3 * g + 3;  // first shard after triple g
-      if (KT - g == 2) {        // triples g (in A) and g + 1, then the remainder
-        b0 = ld(i);
-        b1 = ld(i + 1);
-        b2 = ld(i + 2);
-        __builtin_amdgcn_sched_barrier(0);
+      const int i = G * g + G;  // first shard after group g
+      if (KG - g == 2) {        // groups g (in A) and g + 1, then the remainder
+        load_g(B, i);
         if (rem == 0) {
-          mac3(a0, a1, a2, g);
-          mac3(b0, b1, b2, g + 1);
+          mac_g(A, G * g, G);
+          mac_g(B, i, G);
         } else if (rem == 1) {
-          mac3(a0, a1, a2, g);
-          a0 = ld(i + 3);
-          __builtin_amdgcn_sched_barrier(0);
-          mac3(b0, b1, b2, g + 1);
-          mac_rem(a0, a0, 1);
+          mac_g(A, G * g, G);
+          load_rem(A, i + G, 1);
+          mac_g(B, i, G);
+          mac_g(A, i + G, 1);
         } else {
-          mac3(a0, a1, a2, g);
-          a0 = ld(i + 3);
-          a1 = ld(i + 4);
-          __builtin_amdgcn_sched_barrier(0);
-          mac3(b0, b1, b2, g + 1);
-          mac_rem(a0, a1, 2);
+          mac_g(A, G * g, G);
+          load_rem(A, i + G, 2);
+          mac_g(B, i, G);
+          mac_g(A, i + G, 2);
         }
-      } else {  // triple g (in A), then the remainder
+      } else {  // group g (in A), then the remainder
         if (rem == 0) {
-          mac3(a0, a1, a2, g);
+          mac_g(A, G * g, G);
         } else if (rem == 1) {
-          b0 = ld(i);
-          __builtin_amdgcn_sched_barrier(0);
-          mac3(a0, a1, a2, g);
-          mac_rem(b0, b0, 1);
+          load_rem(B, i, 1);
+          mac_g(A, G * g, G);
+          mac_g(B, i, 1);
         } else {
-          b0 = ld(i);
-          b1 = ld(i + 1);
-          __builtin_amdgcn_sched_barrier(0);
-          mac3(a0, a1, a2, g);
-          mac_rem(b0, b1, 2);
+          load_rem(B, i, 2);
+          mac_g(A, G * g, G);
+          mac_g(B, i, 2);
         }
       }
     } else if constexpr (P::WIX) {

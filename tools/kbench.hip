@@ -436,14 +436,16 @@ int main(int argc, char** argv) {
   }
   if ((m == 2 || m == 3 || m == 4 || m == 8) && std::getenv("KB_TRIDB")) {
     // triple-loop forms: WIX 2 (production), 4 (loads past K leave zeros), 3 (two register
-    // sets, no conditional loads), 3 at <= 80 VGPRs; orders X32, G2, Q16
+    // sets, no conditional loads), 3 at <= 80 VGPRs, 5 (pairs in two register sets);
+    // orders X32, G2, Q16
 #define KB_TW(R, ORD, WX, WP) Policy<(WP), 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, WX>
 #define KB_TV(R, ORD, WX, WP, NAME) \
   vs.push_back(Variant{NAME, [](const ApplyArgs& a, hipStream_t s) { launch_lds<R, KB_TW(R, ORD, WX, WP)>(a, s); }});
 #define KB_TVS(R, WP8)                                                                            \
   KB_TV(R, 11, 2, WP8, "tri2 x32") KB_TV(R, 11, 4, WP8, "tri4 x32") KB_TV(R, 11, 3, 2, "tridb x32") \
   KB_TV(R, 11, 3, 6, "tridb6 x32") KB_TV(R, 5, 2, WP8, "tri2 g2") KB_TV(R, 5, 4, WP8, "tri4 g2")    \
-  KB_TV(R, 5, 3, 2, "tridb g2") KB_TV(R, 8, 2, WP8, "tri2 q16") KB_TV(R, 8, 3, 2, "tridb q16")
+  KB_TV(R, 5, 3, 2, "tridb g2") KB_TV(R, 8, 2, WP8, "tri2 q16") KB_TV(R, 8, 3, 2, "tridb q16")      \
+  KB_TV(R, 11, 5, 2, "pairdb x32") KB_TV(R, 5, 5, 2, "pairdb g2")
     switch (m) {
       case 2: KB_TVS(2, 8) break;
       case 3: KB_TVS(3, 8) break;
