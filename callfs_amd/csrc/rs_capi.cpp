@@ -892,10 +892,20 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   // staging copies, no chunk pipeline, nothing for the CPU but the join of present
   // data shards. RS(10,4) 64 MiB: 43.7 GiB/s vs 36.7 for H2D + launch + D2H
   // (tests/perf/zerocopy_probe.py).
-  static const unsigned long long zc_min = [] {
+  // Threshold: 48 KiB per shard over the call (S x batch), i.e. 48 KiB x n over all n
+  // shards. Below it the one-dispatch path on the library's coherent staging is faster;
+  // tools/zc_threshold.sh (profiles/r04/zc_threshold/zc.jsonl, GiB/s enc / dec, 1 thread,
+  // zero-copy vs one-dispatch): RS(4,2) 128 KiB objects 4.6 / 4.2 vs 6.2 / 5.9, 256 KiB
+  // 8.7 / 7.7 vs 5.3 / 5.3; RS(10,4) 384 KiB 9.6 / 8.9 vs 9.0 / 9.1, 512 KiB 11.7 / 11.4 vs
+  // 8.0 / 10.0; RS(16,4) 512 KiB 11.2 / 9.1 vs 10.9 / 9.2, 1 MiB 20.9 / 17.1 vs 10.8 / 14.6.
+  // (Round 2's 128 KiB over all shards predates the one-dispatch path.)
+  // CALLFS_RS_ZERO_COPY_MIN_BYTES sets it in bytes over all n shards instead.
+  static const long long zc_env = [] {
     const char* e = std::getenv("CALLFS_RS_ZERO_COPY_MIN_BYTES");
-    return e ? std::strtoull(e, nullptr, 0) : (128ull << 10);  // crossover: 80-160 KiB
+    return e ? static_cast<long long>(std::strtoull(e, nullptr, 0)) : -1LL;
   }();
+  const unsigned long long zc_min =
+      zc_env >= 0 ? static_cast<unsigned long long>(zc_env) : (48ull << 10) * static_cast<unsigned long long>(n);
   bool direct = !ctx->pinned.empty() &&
                 static_cast<unsigned long long>(S) * n * batch >= zc_min;
   for (int b = 0; direct && b < batch; ++b) {

@@ -248,13 +248,42 @@ template <int ORD, int... Rs>
 constexpr auto lds_tri_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsTriPolicy<Rs + 1, ORD>>...};
 }
-// [consecutive, G2, X32, Q8, Q16][R - 1] (tri_index)
-const std::array<std::array<VecFn, 8>, 5> kLdsTri = {
+// [consecutive, G2, X32, Q8, Q16, X8][R - 1] (tri_index)
+const std::array<std::array<VecFn, 8>, 6> kLdsTri = {
     lds_tri_table<0>(std::make_integer_sequence<int, 8>{}),
     lds_tri_table<5>(std::make_integer_sequence<int, 8>{}),
     lds_tri_table<11>(std::make_integer_sequence<int, 8>{}),
     lds_tri_table<6>(std::make_integer_sequence<int, 8>{}),
-    lds_tri_table<8>(std::make_integer_sequence<int, 8>{})};
+    lds_tri_table<8>(std::make_integer_sequence<int, 8>{}),
+    lds_tri_table<10>(std::make_integer_sequence<int, 8>{})};
+// The triple loop double-buffered in two register sets with no conditional loads
+// (rs_apply.hpp Policy::WIX 3): the compiler's waits then leave six loads in flight where
+// the rotating form waited for the next triple inside each iteration. 81 VGPRs (5 waves
+// per SIMD) at R <= 4; at R = 8 it needs 131 and lost (3 waves). Launches with R <= 4 and
+// K >= 6 that take the triple form run it. tools/tridb_probe.sh, profiles/r04/tridb/,
+// % of 8 TB/s, rotating -> double-buffered triples in the same order: RS(10,4) 1 MiB 76.6
+// -> 80.0 (G2), RS(8,4) 2 MiB 77.4 -> 80.5 (X32), RS(12,4) 1 MiB 79.4 -> 80.9 (G2),
+// RS(6,3) 1 MiB 75.6 -> 78.4, 4 MiB 75.8 -> 78.1 (X32), RS(6,3) 174,763 B 72.2 -> 75.9,
+// RS(10,4) 16 MiB 77.7 -> 77.9 (Q16); with K = 4 (no loop iteration) it lost 0.5-7 points.
+template <int ORD>
+using LdsTriDbPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, 3>;
+// [consecutive, G2, X32, Q8, Q16, X8][R - 1] (tri_index), R <= 4
+const std::array<std::array<VecFn, 4>, 6> kLdsTriDb = {
+    lds_order_table<LdsTriDbPolicy<0>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbPolicy<5>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbPolicy<11>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbPolicy<6>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbPolicy<8>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbPolicy<10>>(std::make_integer_sequence<int, 4>{})};
+// CALLFS_RS_TRIDB=0 keeps R <= 4 triple launches on the rotating loop (A/B)
+bool tridb_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CALLFS_RS_TRIDB");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+constexpr int kTriDbMinK = 6;
 // [consecutive, G2, X32, Q8, Q16][R - 1] for R <= 4 with Verify rows (tri_index)
 const std::array<std::array<VecFn, 4>, 5> kLdsTriVerify = {
     lds_order_table<LdsTriVerifyPolicy<0>>(std::make_integer_sequence<int, 4>{}),
@@ -413,13 +442,14 @@ bool tri_tunable_launch(const ApplyArgs& a) {
   return wix_enabled() && tri_tunable(a.K, a.R, (a.in_misalign | a.out_misalign) != 0,
                                       (a.verify_mask & rows) != 0, (a.verify_mask & rows) == rows);
 }
-// kLdsTri's first index; orders without a triple instance (G8, X8) are not offered
+// kLdsTri's first index; G8 has no triple instance (tri_order maps it to X32)
 int tri_index(TileOrder o) {
   switch (o) {
     case TileOrder::kGroup2: return 1;
     case TileOrder::kXcd32: return 2;
     case TileOrder::kSeg8: return 3;
     case TileOrder::kSeg16: return 4;
+    case TileOrder::kXcd8: return 5;
     default: return 0;
   }
 }
@@ -516,6 +546,7 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       // tri-G2, profiles/r04/tri_sweep1, tri_sweep2); tri-Q16 above 8 MiB
       if (tps >= 64) add(tri_in(TileOrder::kSeg8));
       if (tps > 1024 || (every_instance && tps >= 64)) add(tri_in(TileOrder::kSeg16));
+      if (tps > 1024 || every_instance) add(tri_in(TileOrder::kXcd8));
     }
     if (every_instance && can_wix(a)) {  // WIX: A/B instances only
       const int n0 = static_cast<int>(c.size());
@@ -580,9 +611,13 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           if (!tri && order < 0 && takes_tri(a)) tri = true;  // the rule: ord is the nibble rule's
           if (tri) {
             const int ti = tri_index(order < 0 ? static_cast<TileOrder>(tri_rule_of(a)) : ord);
-            fn = a.R <= 4 && (a.verify_mask & rows) && (a.verify_mask & rows) != rows
-                     ? kLdsTriVerify[ti][a.R - 1]  // written + Verify rows: early compares
-                     : kLdsTri[ti][a.R - 1];
+            const bool mixed = (a.verify_mask & rows) && (a.verify_mask & rows) != rows;
+            if (a.R <= 4 && mixed)  // written + Verify rows: early compares (no X8 instance)
+              fn = kLdsTriVerify[ti == 5 ? 2 : ti][a.R - 1];
+            else if (a.R <= 4 && a.K >= kTriDbMinK && tridb_enabled())
+              fn = kLdsTriDb[ti][a.R - 1];
+            else
+              fn = kLdsTri[ti][a.R - 1];
           }
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];

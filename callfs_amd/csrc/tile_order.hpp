@@ -130,14 +130,10 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
 }
 
 // The triple form's tile order for the order the nibble rule (or CALLFS_RS_TILE_ORDER)
-// picks: G8 (shards up to 256 KiB) and X8 -> X32, which ran within 0.6 points of G8 for the
-// 6-bit form at 1 MiB objects; every other order has its own triple instance.
+// picks: G8 (shards up to 256 KiB) -> X32, which ran within 0.6 points of G8 for the 6-bit
+// form at 1 MiB objects; every other order has its own triple instance.
 inline TileOrder tri_order(TileOrder nibble) {
-  switch (nibble) {
-    case TileOrder::kGroup8:
-    case TileOrder::kXcd8: return TileOrder::kXcd32;
-    default: return nibble;
-  }
+  return nibble == TileOrder::kGroup8 ? TileOrder::kXcd32 : nibble;
 }
 
 // Triple-load form of an aligned R <= 8 LDS launch (Policy::WIX 2, rs_kernels.hip
@@ -182,7 +178,10 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
   }
   if (tps <= 32) return K <= 6 || R >= 5 ? x32 : -1;
   if (read_only) return x32;
-  if (K <= 5) return x32;
+  // K <= 5 above 8 MiB: X8 (tools/triord_probe.sh, profiles/r04/triord/: RS(4,2) 16 MiB
+  // 71.7 -> 81.1, 32 MiB 77.5 -> 81.4, 16 MiB at a padded pitch 76.6 -> 80.4; 8 MiB X32
+  // 80.9 vs X8 79.4)
+  if (K <= 5) return tps > 1024 ? static_cast<int>(TileOrder::kXcd8) : x32;
   if (K == 6) return tps <= 256 ? x32 : q16;
   if (addr_tz >= 24 && S >= (16ull << 20) && S <= (32ull << 20)) return q16;
   if (tps <= 256) return static_cast<int>(tri_order(nibble));

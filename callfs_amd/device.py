@@ -142,7 +142,7 @@ class Plan:
                    6: "x32", 32: "realign", 37: "realign-x8", 38: "realign-x32",
                    64: "wix", 65: "wix-g8", 66: "wix-g2", 67: "wix-q8", 68: "wix-q16",
                    69: "wix-x8", 70: "wix-x32", 96: "tri", 98: "tri-g2", 99: "tri-q8",
-                   100: "tri-q16", 102: "tri-x32", 128: "realign-tri", 133: "realign-tri-x8",
+                   100: "tri-q16", 101: "tri-x8", 102: "tri-x32", 128: "realign-tri", 133: "realign-tri-x8",
                    134: "realign-tri-x32"}
 
     def tune(self, reps: int = 5, stream: Optional[torch.cuda.Stream] = None) -> list:

@@ -1191,7 +1191,7 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
     plain = {"consecutive", "g8", "g2", "q8", "q16", "x8", "x32"}
     # an encode plan with R <= 8 rows and 3..12 inputs may also take the triple loads
     tri_ok = 3 <= k <= 16 and m <= 8
-    allowed = plain | ({"tri", "tri-g2", "tri-x32", "tri-q8", "tri-q16"} if tri_ok else set())
+    allowed = plain | ({"tri", "tri-g2", "tri-x32", "tri-q8", "tri-q16", "tri-x8"} if tri_ok else set())
     assert all(n in allowed for n in names), names
     sb.fill_random(S + k + 1)  # fresh data: the tuned plan must compute it, not reuse
     enc.launch()
@@ -1223,7 +1223,7 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
 ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign",
                    "realign-x8", "realign-x32", "wix", "wix-g8", "wix-g2", "wix-q8", "wix-q16",
                    "wix-x8", "wix-x32", "tri", "tri-g2", "tri-x32", "tri-q8", "tri-q16",
-                   "realign-tri", "realign-tri-x8", "realign-tri-x32"]
+                   "tri-x8", "realign-tri", "realign-tri-x8", "realign-tri-x32"]
 
 
 @pytest.mark.parametrize("k,m,S,batch,off,erase", [
@@ -1632,3 +1632,30 @@ def test_ragged_tail_wave_placement(native_lib, k, m, S):
     sb.buf[1, n - 1, S - 1] ^= 0x20
     dec.launch()
     assert dec.corrupt_stripes() == [1]
+
+
+@pytest.mark.parametrize("k", [6, 7, 8, 9, 10, 11, 12, 13, 15, 16])
+@pytest.mark.parametrize("m", [1, 2, 4])
+def test_plan_double_buffered_triples_vs_oracle(native_lib, k, m):
+    """R <= 4 launches with K >= 6 run the triple loop double-buffered in two register sets
+    (Policy::WIX 3): its straight-line tails cover one or two remaining triples and K % 3 =
+    0, 1, 2 leftover shards. Every form, in three orders with triple instances, against the
+    oracle on every byte of every stripe, with a ragged tail."""
+    import torch
+    from callfs_amd.device import Plan
+    S, batch, n = 65_536 + 16 * 37 + 5, 3, k + m
+    pitch = (S + 255) // 256 * 256
+    buf = torch.randint(0, 256, (batch, n, pitch), dtype=torch.uint8, device="cuda:0")
+    ptrs = [buf[b, i].data_ptr() for b in range(batch) for i in range(n)]
+    h = buf.cpu().numpy()
+    want = [cref.encode([h[b, i, :S] for i in range(k)], k, m) for b in range(batch)]
+    for order in ("tri", "tri-g2", "tri-x8"):
+        buf[:, k:].zero_()
+        plan = Plan(k, m, S, batch, ptrs)
+        plan.set_orders([order])
+        plan.launch()
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy()
+        for b in range(batch):
+            for j in range(m):
+                assert np.array_equal(got[b, k + j, :S], want[b][j]), (order, b, j)

@@ -75,6 +75,8 @@ def test_lds_kernel_occupancy(kernels):
             want = 7 if r <= 4 else 5
         elif triple and vpf:  # triples with early compares (R <= 4): 67-75 VGPRs
             want = 6
+        elif _policy(k)[14] == "3":  # double-buffered triples (R <= 4): 81 VGPRs
+            want = 5
         else:
             want = 8 if r <= 4 else (6 if realign else 5 if triple else 7) if r <= 8 else 4
         assert k["waves_per_simd"] >= want, (k["name"], k["vgprs"], k["waves_per_simd"])

@@ -13,6 +13,6 @@ for sh in "${shapes[@]}"; do
   IFS=, read k m S <<< "$sh"
   B=$(( (4 << 30) / (S * (k + m)) )); [ $B -lt 1 ] && B=1
   timeout -k 10 300 python -u tools/order_ab.py --rounds 4 \
-    --orders consecutive,g2,q8,q16,x32,tri,tri-g2,tri-x32,tri-q8,tri-q16 \
+    --orders consecutive,g2,q8,q16,x32,tri,tri-g2,tri-x32,tri-q8,tri-q16,tri-x8 \
     --shape $k,$m,$S,$B >> "$OUT/ab.jsonl" 2>> "$OUT/ab.err" || exit $?
 done
