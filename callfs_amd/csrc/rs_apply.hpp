@@ -114,7 +114,7 @@ struct Policy {
   // (WIX 2 with REALIGN: the realigning kernel's aligned loads issued in triples)
   static constexpr int WIX = WIX_;
   // (WIX 2 with VPF: the aligned triple loop with early compare loads)
-  static_assert(!WIX_ || ((REALIGN_ == 0 || WIX_ == 2) && (VPF_ == 0 || (WIX_ == 2 && REALIGN_ == 0)) &&
+  static_assert(!WIX_ || ((REALIGN_ == 0 || WIX_ == 2) && (VPF_ == 0 || ((WIX_ == 2 || WIX_ == 3) && REALIGN_ == 0)) &&
                           RING_ == 0 && !NOMATH_ && !SDWA_),
                 "WIX: ring-of-three kernel only; 6-bit lookups on aligned shards only");
   // > 0: Verify rows' stored vectors are loaded VPF shards before the end of the input
@@ -892,6 +892,16 @@ void rs_apply_lds(ApplyArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);
       };
+      // VPF: the Verify rows' compare loads go out with the loads of the last groups
+      auto load_vpf = [&]() {
+        if constexpr (kVpf) {
+#pragma unroll
+          for (int r = 0; r < RT; ++r)
+            if (r < R && ((a.verify_mask >> r) & 1u))
+              vpre[r] = load16<P>(reinterpret_cast<const uint4*>(out[r]) + v0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
       load_g(A, 0);
       int g = 0;
 #pragma unroll 1
@@ -904,6 +914,7 @@ void rs_apply_lds(ApplyArgs a) {
       const int i = G * g + G;  // first shard after group g
       if (KG - g == 2) {        // groups g (in A) and g + 1, then the remainder
         load_g(B, i);
+        load_vpf();
         if (rem == 0) {
           mac_g(A, G * g, G);
           mac_g(B, i, G);
@@ -920,13 +931,16 @@ void rs_apply_lds(ApplyArgs a) {
         }
       } else {  // group g (in A), then the remainder
         if (rem == 0) {
+          load_vpf();
           mac_g(A, G * g, G);
         } else if (rem == 1) {
           load_rem(B, i, 1);
+          load_vpf();
           mac_g(A, G * g, G);
           mac_g(B, i, 1);
         } else {
           load_rem(B, i, 2);
+          load_vpf();
           mac_g(A, G * g, G);
           mac_g(B, i, 2);
         }

@@ -275,6 +275,18 @@ const std::array<std::array<VecFn, 4>, 6> kLdsTriDb = {
     lds_order_table<LdsTriDbPolicy<6>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsTriDbPolicy<8>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsTriDbPolicy<10>>(std::make_integer_sequence<int, 4>{})};
+// ... with the Verify rows' compare loads issued with the last groups' loads (Policy::VPF):
+// R <= 4 launches that mix written and Verify rows (one-erasure decodes), K >= 6; 92-96
+// VGPRs at 5 waves per SIMD
+template <int ORD>
+using LdsTriDbVerifyPolicy = dev::Policy<5, 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 4, 3>;
+const std::array<std::array<VecFn, 4>, 6> kLdsTriDbVerify = {
+    lds_order_table<LdsTriDbVerifyPolicy<0>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbVerifyPolicy<5>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbVerifyPolicy<11>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbVerifyPolicy<6>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbVerifyPolicy<8>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbVerifyPolicy<10>>(std::make_integer_sequence<int, 4>{})};
 // CALLFS_RS_TRIDB=0 keeps R <= 4 triple launches on the rotating loop (A/B)
 bool tridb_enabled() {
   static const bool on = [] {
@@ -612,9 +624,10 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           if (tri) {
             const int ti = tri_index(order < 0 ? static_cast<TileOrder>(tri_rule_of(a)) : ord);
             const bool mixed = (a.verify_mask & rows) && (a.verify_mask & rows) != rows;
-            if (a.R <= 4 && mixed)  // written + Verify rows: early compares (no X8 instance)
-              fn = kLdsTriVerify[ti == 5 ? 2 : ti][a.R - 1];
-            else if (a.R <= 4 && a.K >= kTriDbMinK && tridb_enabled())
+            const bool db = a.K >= kTriDbMinK && tridb_enabled();
+            if (a.R <= 4 && mixed)  // written + Verify rows: early compares
+              fn = db ? kLdsTriDbVerify[ti][a.R - 1] : kLdsTriVerify[ti == 5 ? 2 : ti][a.R - 1];
+            else if (a.R <= 4 && db)
               fn = kLdsTriDb[ti][a.R - 1];
             else
               fn = kLdsTri[ti][a.R - 1];

@@ -73,10 +73,10 @@ def test_lds_kernel_occupancy(kernels):
         vpf = _policy(k)[13] not in ("0",)  # early compare loads: one uint4 per Verify row
         if realign and triple:  # realigning triples: 67 VGPRs at R <= 4, 94 at R 5..8
             want = 7 if r <= 4 else 5
+        elif _policy(k)[14] == "3":  # double-buffered triples (R <= 4): 81-96 VGPRs
+            want = 5
         elif triple and vpf:  # triples with early compares (R <= 4): 67-75 VGPRs
             want = 6
-        elif _policy(k)[14] == "3":  # double-buffered triples (R <= 4): 81 VGPRs
-            want = 5
         else:
             want = 8 if r <= 4 else (6 if realign else 5 if triple else 7) if r <= 8 else 4
         assert k["waves_per_simd"] >= want, (k["name"], k["vgprs"], k["waves_per_simd"])
