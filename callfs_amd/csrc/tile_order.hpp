@@ -136,54 +136,71 @@ inline TileOrder tri_order(TileOrder nibble) {
   return nibble == TileOrder::kGroup8 ? TileOrder::kXcd32 : nibble;
 }
 
-// Triple-load form of an aligned R <= 8 LDS launch (Policy::WIX 2, rs_kernels.hip
-// takes_tri; DESIGN.md §5 "Shard triples"): the loads of three input shards issued
-// together, then their nibble lookups. Returns the triple form's tile order (instances:
-// consecutive, G2, X32, Q8, Q16), or -1 for the ring of three in the nibble rule's order
-// `nibble`.
-//
-// Round 3 (tools/profile_sweep.sh, profiles/r03/r03s5 and r03s6): launches that write every
-// row or compare every row, shards up to 2 MiB, up to 4 MiB with K <= 6, and at <= 256 KiB
-// only K <= 6 or R >= 5, in the nibble rule's order (G8 -> X32): RS(4,2) 1 MiB 72 -> 80.6,
-// RS(10,8) 74.4 -> 78.2, RS(12,4) 77.2 -> 80.3.
-// Round 4 (tools/tri_sweep.sh, profiles/r04/tri_sweep1 and tri_sweep2, two runs; shapes
-// outside the fit in profiles/r04/tri_validate; % of 8 TB/s, round-3 rule -> this rule):
-//  * write every row, K <= 5: X32 at every size above 256 KiB: RS(4,2) 1 MiB 79.2 -> 81.0,
-//    2 MiB 81.0 -> 84.1, 4 MiB 77.9 -> 80.2, 8 MiB 70.0 -> 79.6, 16 MiB 69.9 -> 72.9,
-//    32 MiB 69.8 -> 78.0, 64 MiB 71.5 -> 82.2; RS(5,3) 8 MiB 71.2 -> 77.9, 16 MiB 70.4 -> 75.7;
-//  * write every row, K = 6: X32 up to 2 MiB, Q16 above: RS(6,3) 1 MiB 74.6 -> 75.3,
-//    2.8 MB 74.1 -> 77.6, 4 MiB 71.7 -> 77.3, 8 MiB 73.2 -> 74.5, 11.2 MB 73.3 -> 75.2,
-//    16 MiB 73.2 -> 76.5, 32 MiB 73.8 -> 76.4; RS(6,6) 16 MiB 73.0 -> 74.0;
-//  * write every row, K = 7..12 on power-of-two pitches of 16-32 MiB (addr_tz >= 24): Q16:
-//    RS(8,4) 16 MiB 74.1 -> 77.7, RS(10,4) 74.0 -> 77.5, RS(12,4) 71.8 -> 77.4, RS(9,3)
-//    74.6 -> 77.5; elsewhere round 3's rule;
-//  * compare every row (the download's Verify with nothing lost): X32 at every size above
-//    256 KiB: RS(4,2) 8 MiB 82.7 -> 90.5, RS(6,3) 16 MiB 85.7 -> 90.0, RS(8,4) 8 MiB 85.7 ->
-//    88.1, RS(10,4) 4 MiB 84.9 -> 86.3, 16 MiB 84.4 -> 87.8;
-//  * R <= 4 with written and Verify rows (the one-erasure decode), the kernel with early
-//    compare loads (Policy::VPF): K <= 4 in X32 (RS(4,2) 1 MiB erase {1} 76.2 -> 80.1,
-//    4 MiB {0} 76.7 -> 81.1), K 5..12 up to 1 MiB in the nibble rule's order (G2: RS(6,3)
-//    {2} 74.2 -> 75.0, RS(8,4) {5} 77.5 -> 78.3, RS(12,4) {7} 74.4 -> 75.7, RS(10,4) {5}
-//    / {13} / {0} +0.2 / +0.1 / -0.8); larger shards keep the ring (RS(10,4) 6.7 MB {5}
-//    76.3 -> 74.5 in triples).
+// Triple-load form of an aligned R <= 8 LDS launch (rs_kernels.hip takes_tri; DESIGN.md §5
+// "Shard triples", "Round 4"): the loads of three input shards issued together, then their
+// nibble lookups; with R <= 4 and K >= 6 double-buffered in two register sets
+// (Policy::WIX 3), else rotating (WIX 2). Returns the triple form's tile order (instances:
+// consecutive, G2, X32, Q8, Q16, X8), or -1 for the ring of three in the nibble rule's
+// order `nibble`. % of 8 TB/s below, the previous rule -> this one:
+//  * round 3 (profiles/r03/r03s5, r03s6): launches that write every row or compare every
+//    row, shards up to 2 MiB (4 MiB with K <= 6), at <= 256 KiB only K <= 6 or R >= 5, in
+//    the nibble rule's order (G8 -> X32): RS(4,2) 1 MiB 72 -> 80.6, RS(10,8) 74.4 -> 78.2;
+//  * round 4, rotating form (tools/tri_sweep.sh, profiles/r04/tri_sweep1, tri_sweep2,
+//    tri_validate, triord): K <= 5 in X32 up to 8 MiB and X8 above (RS(4,2) 8 MiB 70.0 ->
+//    79.6, 16 MiB 69.9 -> 81.1, 32 MiB 69.8 -> 81.4); R 5..8 with K = 6 in X32 / Q16;
+//    read-only launches in X32 at every size (RS(6,3) 16 MiB 85.7 -> 90.0, RS(10,4) 4 MiB
+//    84.9 -> 86.3); Q16 on 16-32 MiB power-of-two pitches for K 7..12;
+//  * round 4, double-buffered form, R <= 4 and K >= 6 (profiles/r04/tri_sweep3,
+//    tridb_wide): X32 up to 256 KiB (RS(12,4) 87 KB 70.9 -> 75.6, RS(32,4) 32 KiB 67.8 ->
+//    79.3, RS(20,4) 52 KB 68.1 -> 72.2); K = 6 in X32 to 8 MiB, X8 above (RS(6,3) 1 MiB 74.5
+//    -> 78.7, 8 MiB 73.0 -> 78.0, 16 MiB 72.8 -> 77.7); K >= 7 in G2 to 1 MiB (RS(10,4)
+//    76.5 -> 80.0, RS(16,4) 76.5 -> 78.4, RS(32,4) 74.2 -> 76.0), Q8 to 2 MiB (RS(8,4) 77.0
+//    -> 80.7, RS(10,4) 1.68 MB 74.4 -> 78.8), Q8 to 8 MiB for K <= 12 (RS(10,4) 6.7 MB 73.0
+//    -> 76.9, RS(12,4) 5.6 MB 73.8 -> 76.2, RS(8,4) 8 MiB 74.4 -> 75.0), Q16 on 16-32 MiB
+//    power-of-two pitches (RS(10,4) 73.8 -> 78.7); K > 12 above 2 MiB keeps the ring
+//    (RS(16,4) 4 MiB: consecutive 76.0 vs 72.5);
+//  * written + Verify rows (the one-erasure decode), R <= 4, the early-compare forms: K <= 4
+//    in X32 (RS(4,2) erase {1} 76.2 -> 80.1); K = 5 up to 1 MiB in the nibble rule's order;
+//    K 6..16 double-buffered in G2 to 1 MiB and X32 above (profiles/r04/tri_verify_ab2:
+//    RS(10,4) {5} 75.0 -> 77.2, RS(12,4) {7} 74.4 -> 77.3, RS(16,4) {3} 74.6 -> 77.5,
+//    RS(10,4) 6.7 MB {5} 73.8 -> 75.9).
 inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_only,
                           uint64_t tps, int addr_tz, uint64_t S, TileOrder nibble) {
-  if (R > 8 || K < 4 || K > 12 || misaligned) return -1;
-  const int x32 = static_cast<int>(TileOrder::kXcd32), q16 = static_cast<int>(TileOrder::kSeg16);
-  if (verify && !read_only) {  // written + Verify rows: only the R <= 4 early-compare form
+  if (R > 8 || K < 4 || misaligned) return -1;
+  const int x32 = static_cast<int>(TileOrder::kXcd32), q16 = static_cast<int>(TileOrder::kSeg16),
+            q8 = static_cast<int>(TileOrder::kSeg8), x8 = static_cast<int>(TileOrder::kXcd8),
+            g2 = static_cast<int>(TileOrder::kGroup2);
+  const bool pow2_16_32 = addr_tz >= 24 && S >= (16ull << 20) && S <= (32ull << 20);
+  // R <= 4 with K >= 6 runs the double-buffered form (rs_kernels.hip kTriDbMinK)
+  const bool db = R <= 4 && K >= 6;
+  if (verify && !read_only) {  // written + Verify rows: only the R <= 4 early-compare forms
     if (R > 4) return -1;
     if (K <= 4) return x32;
-    if (tps <= 32) return K <= 6 ? x32 : -1;  // as for written rows at small S
+    if (db) {  // round 4 (profiles/r04/tri_verify_ab2): G2 up to 1 MiB, X32 above
+      if (K > 16 || tps <= 32) return tps <= 32 && K <= 6 ? x32 : -1;
+      return tps <= 128 ? g2 : x32;
+    }
+    if (tps <= 32) return x32;
     return tps <= 128 ? static_cast<int>(tri_order(nibble)) : -1;
   }
+  if (db && !read_only) {  // round 4, double-buffered (profiles/r04/tri_sweep3, tridb_wide)
+    if (tps <= 32) return x32;
+    if (K == 6) return tps <= 1024 ? x32 : x8;
+    if (tps <= 128) return g2;
+    if (tps <= 256) return q8;
+    if (K > 12) return -1;  // 2 MiB and up with K > 12: the ring (RS(16,4) 4 MiB)
+    if (tps <= 1024) return q8;
+    return pow2_16_32 ? q16 : -1;
+  }
+  if (K > 12) return -1;
   if (tps <= 32) return K <= 6 || R >= 5 ? x32 : -1;
   if (read_only) return x32;
   // K <= 5 above 8 MiB: X8 (tools/triord_probe.sh, profiles/r04/triord/: RS(4,2) 16 MiB
   // 71.7 -> 81.1, 32 MiB 77.5 -> 81.4, 16 MiB at a padded pitch 76.6 -> 80.4; 8 MiB X32
   // 80.9 vs X8 79.4)
-  if (K <= 5) return tps > 1024 ? static_cast<int>(TileOrder::kXcd8) : x32;
+  if (K <= 5) return tps > 1024 ? x8 : x32;
   if (K == 6) return tps <= 256 ? x32 : q16;
-  if (addr_tz >= 24 && S >= (16ull << 20) && S <= (32ull << 20)) return q16;
+  if (pow2_16_32) return q16;
   if (tps <= 256) return static_cast<int>(tri_order(nibble));
   return -1;
 }
@@ -203,7 +220,7 @@ inline bool realign_tri_rule(int K, int R, bool verify, bool read_only) {
 // (R <= 4 launches that mix written and Verify rows take the triple loop with early
 // compare loads, Policy::VPF)
 inline bool tri_tunable(int K, int R, bool misaligned, bool verify, bool read_only) {
-  return R <= 8 && K >= 3 && K <= 16 && !misaligned && (!verify || read_only || R <= 4);
+  return R <= 8 && K >= 3 && (K <= 16 || R <= 4) && !misaligned && (!verify || read_only || R <= 4);
 }
 // Wide groups hold 19-32 shard streams per stripe; from 2 MiB shards on, 8 interleaved
 // column segments beat consecutive tiles (tools/order_sweep.sh, KB_ORD, 9 rounds, % of

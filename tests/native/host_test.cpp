@@ -304,7 +304,8 @@ int main() {
     CHECK(tri_rule(4, 2, false, true, true, t1));     // download Verify (read-only)
     CHECK(!tri_rule(3, 2, false, false, false, t1));  // k = 3: the v_perm kernel
     CHECK(tri_rule(12, 4, false, false, false, t1));
-    CHECK(!tri_rule(16, 4, false, false, false, t1)); // the tuner decides
+    CHECK(tri_rule(16, 4, false, false, false, t1));  // double-buffered from K = 6 at R <= 4
+    CHECK(!tri_rule(16, 8, false, false, false, t1)); // rotating form: K <= 12
     CHECK(!tri_rule(4, 2, true, false, false, t1));   // Split layout: realigning kernel
     CHECK(tri_rule(6, 3, false, true, false, t1));    // written + Verify rows: early compares
     CHECK(!tri_rule(6, 6, false, true, false, t1));   // ... at R <= 4 only
@@ -312,17 +313,20 @@ int main() {
     CHECK(!tri_rule(8, 8, false, false, false, tps_of(8 * MiB)));     // 8 MiB shards: lost
     CHECK(tri_rule(8, 4, false, false, false, tps_of(2 * MiB)));      // 2 MiB: gained
     CHECK(tri_rule(4, 2, false, false, false, tps_of(256 << 10)));    // small S, few inputs
-    CHECK(!tri_rule(10, 4, false, false, false, tps_of(104858)));     // small S, 10 inputs
+    CHECK(tri_rule(10, 4, false, false, false, tps_of(104858)));      // small S, double-buffered
     CHECK(tri_rule(10, 8, false, false, false, tps_of(104858)));      // small S, R = 8
-    CHECK(!tri_rule(10, 4, false, false, false, tps_of(4 * MiB)));
-    CHECK(!tri_rule(10, 4, false, false, false, tps_of(6710887)));    // configs[2] shards
+    CHECK(tri_rule(10, 4, false, false, false, tps_of(4 * MiB)));     // double-buffered, Q8
+    CHECK(tri_rule(10, 4, false, false, false, tps_of(6710887)));     // configs[2] shards
+    CHECK(!tri_rule(16, 4, false, false, false, tps_of(4 * MiB)));    // K > 12 above 2 MiB
     // round 4: K <= 5 in X32 up to 8 MiB (RS(4,2) 8 MiB 70.0 -> 79.6), X8 above (16 MiB
     // 71.7 -> 81.1, 32 MiB 77.5 -> 81.4)
     const int X8 = static_cast<int>(TileOrder::kXcd8);
     CHECK(tro(4, 2, MiB, 20) == X32 && tro(4, 2, 8 * MiB, 23) == X32 && tro(4, 2, 5592406, 8) == X32);
     CHECK(tro(4, 2, 16 * MiB, 24) == X8 && tro(4, 2, 64 * MiB, 26) == X8 && tro(5, 3, 16 * MiB, 24) == X8);
     // K 5..6: X32 up to 2 MiB, Q16 above (RS(6,3) 4 MiB 71.7 -> 77.3, 16 MiB 73.2 -> 76.5)
-    CHECK(tro(6, 3, MiB, 20) == X32 && tro(6, 3, 2796203, 8) == Q16 && tro(6, 3, 16 * MiB, 24) == Q16);
+    CHECK(tro(6, 3, MiB, 20) == X32 && tro(6, 3, 2796203, 8) == X32 && tro(6, 3, 16 * MiB, 24) == X8);
+    CHECK(tro(6, 6, 2796203, 8) == Q16);  // R 5..8: the rotating form's K = 6 rule
+    CHECK(tro(10, 4, 104858, 8) == X32 && tro(10, 4, 1677722, 8) == static_cast<int>(TileOrder::kSeg8));
     // K 7..12: Q16 on 16-32 MiB power-of-two pitches, round 3's rule elsewhere
     CHECK(tro(10, 4, 16 * MiB, 24) == Q16 && tro(12, 4, 32 * MiB, 25) == Q16);
     CHECK(tro(10, 4, 16 * MiB, 8) == -1 && tro(10, 4, 64 * MiB, 26) == -1);
@@ -331,9 +335,11 @@ int main() {
     CHECK(tro(4, 2, 16 * MiB, 24, true, true) == X32 && tro(10, 4, MiB, 20, true, true, TileOrder::kXcd32) == X32);
     // written + Verify rows (R <= 4, early compares): K <= 4 in X32, K 5..12 up to 1 MiB
     CHECK(tro(4, 2, MiB, 20, true, false) == X32 && tro(4, 2, 4 * MiB, 22, true, false) == X32);
-    CHECK(tro(10, 4, MiB, 20, true, false) == G2 && tro(10, 4, 6710887, 8, true, false) == -1);
+    CHECK(tro(10, 4, MiB, 20, true, false) == G2 && tro(10, 4, 6710887, 8, true, false) == X32);
+    CHECK(tro(5, 3, 6710887, 8, true, false) == -1 && tro(20, 4, MiB, 20, true, false) == -1);
     CHECK(tro(10, 4, 104858, 8, true, false) == -1 && tro(6, 3, 174763, 8, true, false) == X32);
-    CHECK(tri_tunable(16, 4, false, false, false) && !tri_tunable(20, 4, false, false, false));
+    CHECK(tri_tunable(16, 4, false, false, false) && tri_tunable(20, 4, false, false, false) &&
+          !tri_tunable(20, 8, false, false, false));  // R <= 4: the double-buffered form at any K
     CHECK(tri_order(TileOrder::kGroup8) == TileOrder::kXcd32);
     CHECK(tri_order(TileOrder::kGroup2) == TileOrder::kGroup2);
     CHECK(tri_order(TileOrder::kConsecutive) == TileOrder::kConsecutive);

@@ -1634,7 +1634,7 @@ def test_ragged_tail_wave_placement(native_lib, k, m, S):
     assert dec.corrupt_stripes() == [1]
 
 
-@pytest.mark.parametrize("k", [6, 7, 8, 9, 10, 11, 12, 13, 15, 16])
+@pytest.mark.parametrize("k", [6, 7, 8, 9, 10, 11, 12, 13, 15, 16, 32, 65])
 @pytest.mark.parametrize("m", [1, 2, 4])
 def test_plan_double_buffered_triples_vs_oracle(native_lib, k, m):
     """R <= 4 launches with K >= 6 run the triple loop double-buffered in two register sets
