@@ -45,8 +45,9 @@ struct ApplyArgs {
   // the same over the launch group's output (written or compared) shard pointers; with
   // in_misalign it selects the form that also aligns the parity stores (REALIGN 2)
   uint32_t out_misalign;
-  // set by launch_apply: the vector kernel's first tile per stripe also computes the ragged
-  // tail S % 16 (no separate byte-kernel launch)
+  // set by launch_apply: the vector kernel also computes the ragged tail S % 16 (no separate
+  // byte-kernel launch); 1 = in each stripe's first tile, 2 = in the idle last wave of its
+  // last tile where there is one (rs_apply.hpp tail_lane)
   uint32_t tail_in_vec;
 };
 

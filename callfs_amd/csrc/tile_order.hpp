@@ -103,12 +103,20 @@ constexpr int kTileOrders = 7;
 // 81.2 / 81.4, RS(6,3) 2.8 MB 84.8 / 84.6 -> 85.3 / 85.3; at 105 KB shards all orders
 // within 0.3.
 //
+// Round 4 re-measured G2 for many streams above 1 MiB on the current kernels (every order,
+// interleaved, tools/order_ab.py; profiles/r04/tri_sweep1-3, tridb_wide, wide_db, % of
+// 8 TB/s, G2 -> consecutive, runs averaged): with R <= 4 consecutive tiles won on every
+// shape, RS(16,4) 4 MiB 74.2 -> 75.7, RS(14,4) 4.8 MB 71.7 -> 73.6, RS(20,4) 3.4 MB 72.8 ->
+// 74.0, RS(24,4) 2.8 MB 71.0 -> 71.8, RS(12,4) 5.6 MB 74.0 -> 74.9, RS(10,4) 4 MiB 74.3 ->
+// 75.0, RS(16,4) 2 MiB 75.2 -> 75.6; with R = 8 G2 kept its lead (RS(10,8) 6.7 MB 71.5 vs
+// 70.9, RS(8,8) 8 MiB 71.7 vs 69.0). So G2 above 1 MiB only for launches of 5-8 rows.
+//
 // tps = tiles of 512 16-B vectors (8 KiB) per stripe; streams = K + R of the launch;
 // addr_tz / stripe_stride as in ApplyArgs; verify = the launch compares some rows,
-// read_only = it compares every row (writes nothing).
+// read_only = it compares every row (writes nothing); rows = R.
 inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int streams,
                                 uint64_t stripe_stride, bool verify = false,
-                                bool read_only = false) {
+                                bool read_only = false, int rows = 8) {
   if (read_only && tps > 32) return TileOrder::kXcd32;
   // stripes exactly 2 MiB apart: interleaving stripes costs 2-12 points (RS(8,8) 128 KiB
   // 72.4 -> 60.6 with G8, RS(4,4) 256 KiB 77.9 -> 65.8, RS(6,2) 256 KiB 81.5 -> 78.4);
@@ -119,7 +127,7 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
   // -> 67.7, RS(12,4) 64 KiB equal)
   if (stripe_stride == (1ull << 20) && tps <= 32) return TileOrder::kGroup2;
   if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
-  if (tps <= 128 || (tps <= 1024 && streams >= 14 && !verify)) return TileOrder::kGroup2;
+  if (tps <= 128 || (tps <= 1024 && streams >= 14 && rows >= 5 && !verify)) return TileOrder::kGroup2;
   if (tps <= 1024) return TileOrder::kConsecutive;  // S <= 8 MiB, few streams
   if (addr_tz >= 23 && S < (128ull << 20)) {
     if (streams >= 12)
@@ -158,7 +166,10 @@ inline TileOrder tri_order(TileOrder nibble) {
 //    -> 80.7, RS(10,4) 1.68 MB 74.4 -> 78.8), Q8 to 8 MiB for K <= 12 (RS(10,4) 6.7 MB 73.0
 //    -> 76.9, RS(12,4) 5.6 MB 73.8 -> 76.2, RS(8,4) 8 MiB 74.4 -> 75.0), Q16 on 16-32 MiB
 //    power-of-two pitches (RS(10,4) 73.8 -> 78.7); K > 12 above 2 MiB keeps the ring
-//    (RS(16,4) 4 MiB: consecutive 76.0 vs 72.5);
+//    (RS(16,4) 4 MiB: consecutive 76.0 vs 72.5), and so does K > 16 from 256 KiB to 1 MiB
+//    unless the shards sit 64 KiB-aligned apart (profiles/r04/wide_db, regress: RS(20,4)
+//    S = 838,861 at a 256-B pitch, ring in G2 73.2 / 72.9 vs 71.1 / 71.0; RS(24,4) 699,051 B
+//    72.0 vs 70.9; at a 1 MiB pitch the form leads, RS(20,4) 78.1 vs 74.8);
 //  * written + Verify rows (the one-erasure decode), R <= 4, the early-compare forms: K <= 4
 //    in X32 (RS(4,2) erase {1} 76.2 -> 80.1); K = 5 up to 1 MiB in the nibble rule's order;
 //    K 6..16 double-buffered in G2 to 1 MiB and X32 above (profiles/r04/tri_verify_ab2:
@@ -186,7 +197,7 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
   if (db && !read_only) {  // round 4, double-buffered (profiles/r04/tri_sweep3, tridb_wide)
     if (tps <= 32) return x32;
     if (K == 6) return tps <= 1024 ? x32 : x8;
-    if (tps <= 128) return g2;
+    if (tps <= 128) return K > 16 && addr_tz < 16 ? -1 : g2;
     if (tps <= 256) return q8;
     if (K > 12) return -1;  // 2 MiB and up with K > 12: the ring (RS(16,4) 4 MiB)
     if (tps <= 1024) return q8;

@@ -268,9 +268,13 @@ int main() {
     CHECK(lds_tile_order(MiB, tps_of(MiB), 20, 14, 14 * MiB, true, true) == TileOrder::kXcd32);
     CHECK(lds_tile_order(6710887, tps_of(6710887), 8, 14, 14 * 6711040ull, true, true) == TileOrder::kXcd32);
     CHECK(lds_tile_order(104858, tps_of(104858), 8, 14, 14 * 105216ull, true, true) == TileOrder::kGroup8);
-    // RS(4,2) 4 MiB: consecutive (few streams); RS(16,4) 4 MiB: G2
+    // RS(4,2) 4 MiB: consecutive (few streams); RS(12,8) 4 MiB: G2; RS(16,4) 4 MiB:
+    // consecutive (round 4: G2 above 1 MiB only for 5-8 rows)
     CHECK(lds_tile_order(4 * MiB, tps_of(4 * MiB), 22, 6, 24 * MiB) == TileOrder::kConsecutive);
     CHECK(lds_tile_order(4 * MiB, tps_of(4 * MiB), 22, 20, 80 * MiB) == TileOrder::kGroup2);
+    CHECK(lds_tile_order(4 * MiB, tps_of(4 * MiB), 22, 20, 80 * MiB, false, false, 4) ==
+          TileOrder::kConsecutive);
+    CHECK(lds_tile_order(MiB, tps_of(MiB), 20, 20, 20 * MiB, false, false, 4) == TileOrder::kGroup2);
     // power-of-two 16 MiB shards: Q16 with 14 streams, consecutive with 6
     CHECK(lds_tile_order(16 * MiB, tps_of(16 * MiB), 24, 14, 224 * MiB) == TileOrder::kSeg16);
     CHECK(lds_tile_order(16 * MiB, tps_of(16 * MiB), 24, 6, 96 * MiB) == TileOrder::kConsecutive);
@@ -331,6 +335,9 @@ int main() {
     CHECK(tro(10, 4, 16 * MiB, 24) == Q16 && tro(12, 4, 32 * MiB, 25) == Q16);
     CHECK(tro(10, 4, 16 * MiB, 8) == -1 && tro(10, 4, 64 * MiB, 26) == -1);
     CHECK(tro(10, 4, MiB, 20) == G2);  // the nibble rule's order (G2 for the bench shape)
+    // K > 16 from 256 KiB to 1 MiB: the ring on unaligned pitches, G2 on 64 KiB-aligned ones
+    CHECK(tro(20, 4, 838861, 8) == -1 && tro(20, 4, MiB, 20) == G2 && tro(16, 4, 838861, 8) == G2);
+    CHECK(tro(20, 4, 52429, 8) == X32);
     // read-only launches: X32 at every size above 256 KiB (RS(6,3) 16 MiB 85.7 -> 90.0)
     CHECK(tro(4, 2, 16 * MiB, 24, true, true) == X32 && tro(10, 4, MiB, 20, true, true, TileOrder::kXcd32) == X32);
     // written + Verify rows (R <= 4, early compares): K <= 4 in X32, K 5..12 up to 1 MiB

@@ -1604,6 +1604,8 @@ def test_small_path_every_byte_right_after_flag(native_lib, k, m, S, B):
     (10, 4, 16 * (512 * 2 + 448) + 9),  # 448 vectors: the last wave exactly idle
     (10, 4, 16 * (512 * 2 + 449) + 3),  # 449: the last wave holds one vector -> tile 0
     (10, 4, 16 * 40 + 11),              # one partial tile: first and last tile coincide
+    (10, 4, 16 * (512 * 40 + 100) + 7),  # 41 tiles per stripe (> 32): tile 0's wave 0
+    (6, 3, 16 * (512 * 31 + 60) + 1),    # 32 tiles, partial last: the idle last wave
     (3, 2, 16 * (512 + 77) + 13),       # v_perm kernel (k <= 3), partial last tile
     (3, 2, 16 * 1024 + 1),              # v_perm kernel, full last tile
     (12, 8, 16 * (512 * 4 + 300) + 15),  # R = 8, triple loads at this size
@@ -1611,8 +1613,8 @@ def test_small_path_every_byte_right_after_flag(native_lib, k, m, S, B):
 ])
 def test_ragged_tail_wave_placement(native_lib, k, m, S):
     """The S % 16 tail bytes of every stripe go to the idle last wave of the stripe's last
-    tile when that tile is partial, else to wave 0 of its first tile (rs_apply.hpp
-    tail_lane): encode every byte against the oracle, and a decode with Verify rows flags
+    tile when that tile is partial and a stripe has at most 32 tiles, else to wave 0 of its
+    first tile (rs_apply.hpp tail_lane, rs_kernels.hip tail_mode): encode every byte against the oracle, and a decode with Verify rows flags
     a flipped last byte (which only the tail wave computes) in exactly its stripe."""
     import torch
     from callfs_amd.device import Plan
