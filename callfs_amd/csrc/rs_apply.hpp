@@ -202,20 +202,19 @@ __device__ __forceinline__ void mac_one(uint32_t (&acc)[U][RT][4], const uint4 (
 // kernel has registers to spare (R <= 4), 4 otherwise (8 took R = 8 from 68 to 73 VGPRs).
 template <int RT>
 constexpr int tail_loads() { return RT <= 4 ? 8 : 4; }
-// Which wave takes a stripe's ragged tail (S % 16 bytes). mode = ApplyArgs::tail_in_vec:
-// 2 (stripes of few tiles, launch_apply tail_mode): the block's last wave in the stripe's
-// last tile when that wave holds no vectors (the last tile is partial), so no wave that
-// streams vectors waits for the tail's byte loads; otherwise, and in mode 1, wave 0 of the
-// stripe's first tile, whose wait is hidden behind the rest of a long stripe (in the last
-// tile of the grid's last stripe the tail's load chain delays the kernel's end). Returns
-// the thread's byte index in the tail, or ~0u.
-template <int BS, int TV>
-__device__ __forceinline__ uint32_t tail_lane(uint64_t nvec, uint32_t tps, uint32_t tile,
-                                              uint32_t mode) {
-  const uint64_t last = nvec - static_cast<uint64_t>(tps - 1) * TV;  // vectors in the last tile
-  if ((mode & 2u) && last + 64 <= static_cast<uint64_t>(BS))  // the last tile's last wave is idle
-    return tile == tps - 1 && threadIdx.x >= BS - 64 ? threadIdx.x - (BS - 64) : ~0u;
-  return tile == 0 ? threadIdx.x : ~0u;
+// Which wave takes a stripe's ragged tail (S % 16 bytes): ApplyArgs::tail_in_vec, chosen on
+// the host (rs_kernels.hip tail_code) = (tile << 2) | (last wave << 1) | 1. For stripes of
+// few tiles the block's last wave in the stripe's last tile when that wave holds no
+// vectors (the last tile is partial), so no wave that streams vectors waits for the
+// tail's byte loads; otherwise wave 0 of the stripe's first tile, whose wait is hidden
+// behind the rest of a long stripe (in the last tile of the grid's last stripe the tail's
+// load chain delays the kernel's end). Returns the thread's byte index in the tail, or ~0u.
+// (Decided on the host: the 64-bit tile arithmetic in the kernel cost the v_perm kernel's
+// R = 2 instances 4 SGPRs and a wave.)
+template <int BS>
+__device__ __forceinline__ uint32_t tail_lane(uint32_t code, uint32_t tile) {
+  const uint32_t tid0 = (code & 2u) ? BS - 64 : 0u;
+  return tile == (code >> 2) && threadIdx.x >= tid0 ? threadIdx.x - tid0 : ~0u;
 }
 
 template <int RT>
@@ -281,7 +280,7 @@ void rs_apply_vec(ApplyArgs a) {
     cptr<const uint8_t*> in = as_const(a.in_tab) + static_cast<size_t>(stripe) * K;
     cptr<uint8_t*> out = as_const(a.out_tab) + static_cast<size_t>(stripe) * RT;
     if (a.tail_in_vec) {
-      const uint32_t j = tail_lane<BS, BS * U>(a.nvec, tps, tile, a.tail_in_vec);
+      const uint32_t j = tail_lane<BS>(a.tail_in_vec, tile);
       if (j != ~0u) vec_tail<RT>(a, in, out, stripe, tabs, j);
     }
     bool live[U];
@@ -804,7 +803,7 @@ void rs_apply_lds(ApplyArgs a) {
       if (tile == 0) lds_edges<RT>(a, in, out, stripe, lds0);
     } else {
       if (a.tail_in_vec) {
-        const uint32_t j = tail_lane<BS, TV>(a.nvec, tps, tile, a.tail_in_vec);
+        const uint32_t j = tail_lane<BS>(a.tail_in_vec, tile);
         if (j != ~0u) lds_tail<RT>(a, in, out, stripe, lds0, j);
       }
     }

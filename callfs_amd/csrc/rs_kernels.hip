@@ -296,20 +296,22 @@ bool tridb_enabled() {
   return on;
 }
 constexpr int kTriDbMinK = 6;
-// Ragged-tail placement (ApplyArgs::tail_in_vec, rs_apply.hpp tail_lane): the idle last wave
-// of each stripe's last tile for stripes of at most kTailLastMaxTps tiles, else wave 0 of the
-// first tile. Round 4 moved every tail to the last tile (1 MiB-object shards, 7-22 tiles per
-// stripe, gained 0.4-1.3 points); on long stripes that put the grid's last tile behind the
-// tail's load chain (same-box A/B against round 3's build, profiles/r04/regress: RS(20,4)
-// S = 3,355,444, 410 tiles, 73.5 -> 71.8 % with the kernel otherwise unchanged).
-// CALLFS_RS_TAIL_LAST_TPS overrides the bound (A/B).
-uint32_t tail_mode(uint64_t nvec) {
+// Ragged-tail placement (ApplyArgs::tail_in_vec, rs_apply.hpp tail_lane) for a kernel of
+// TV-vector tiles and BS-thread blocks: the idle last wave of each stripe's last tile for
+// stripes of at most kTailLastMaxTps tiles whose last tile leaves that wave idle, else wave
+// 0 of the first tile. Round 4 moved every tail to the last tile (1 MiB-object shards, 7-22
+// tiles per stripe, gained 0.4-1.3 points); on long stripes that put the grid's last tile
+// behind the tail's load chain (tools/tail_ab.sh, profiles/r04/tail_ab: RS(20,4) S =
+// 3,355,444, 410 tiles, first tile 73.8 %, last tile 72.6). CALLFS_RS_TAIL_LAST_TPS
+// overrides the bound (A/B).
+uint32_t tail_code(uint64_t nvec, uint64_t TV, uint64_t BS) {
   static const uint64_t max_tps = [] {
     const char* e = std::getenv("CALLFS_RS_TAIL_LAST_TPS");
     return e && *e ? std::strtoull(e, nullptr, 10) : 32ull;
   }();
-  const uint64_t tps = (nvec + LdsPolicy::TILE_VECS - 1) / LdsPolicy::TILE_VECS;
-  return tps <= max_tps ? 2u : 1u;
+  const uint64_t tps = (nvec + TV - 1) / TV, last = nvec - (tps - 1) * TV;
+  if (tps <= max_tps && last + 64 <= BS) return static_cast<uint32_t>(((tps - 1) << 2) | 3u);
+  return 1u;
 }
 // [consecutive, G2, X32, Q8, Q16][R - 1] for R <= 4 with Verify rows (tri_index)
 const std::array<std::array<VecFn, 4>, 5> kLdsTriVerify = {
@@ -610,7 +612,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
       if (takes_lds(a)) {
         // the LDS kernel's first tile per stripe computes the S % 16 tail itself: an odd-S
         // launch (Split layout) is one kernel, not two back to back
-        a.tail_in_vec = tail0 < a.S ? tail_mode(a.nvec) : 0u;
+        a.tail_in_vec = tail0 < a.S ? tail_code(a.nvec, LdsPolicy::TILE_VECS, LdsPolicy::BS) : 0u;
         if (a.tail_in_vec) tail0 = a.S;
         if (!a.ltabs) return hipErrorInvalidValue;
         size_t lds = dev::lds_bytes(a.K, a.R);
@@ -682,7 +684,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
                    last && !tail_after, a);
         });
       } else {
-        a.tail_in_vec = tail0 < a.S ? tail_mode(a.nvec) : 0u;  // as for the LDS kernel
+        a.tail_in_vec = tail0 < a.S ? tail_code(a.nvec, ProdPolicy::TILE_VECS, ProdPolicy::BS) : 0u;
         if (a.tail_in_vec) tail0 = a.S;
         VecFn fn = kVec[a.R - 1];  // R <= 4 here (R >= kLdsMinRows takes the LDS kernel)
         switch (order >= 0 ? static_cast<TileOrder>(order) : vec_rule(a)) {
@@ -767,7 +769,7 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
     return hipErrorInvalidValue;
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
-  a.tail_in_vec = a.nvec * 16 < a.S ? tail_mode(a.nvec) : 0u;
+  a.tail_in_vec = a.nvec * 16 < a.S ? tail_code(a.nvec, LdsPolicy::TILE_VECS, LdsPolicy::BS) : 0u;
   if (order >= kOrderRealignTri) order = order - kOrderRealignTri + kOrderRealign;
   else if (order >= kOrderTri) order -= kOrderTri;
   if (order >= kOrderWix) order -= kOrderWix;  // bounded by the nibble kernel's traffic

@@ -45,9 +45,9 @@ struct ApplyArgs {
   // the same over the launch group's output (written or compared) shard pointers; with
   // in_misalign it selects the form that also aligns the parity stores (REALIGN 2)
   uint32_t out_misalign;
-  // set by launch_apply: the vector kernel also computes the ragged tail S % 16 (no separate
-  // byte-kernel launch); 1 = in each stripe's first tile, 2 = in the idle last wave of its
-  // last tile where there is one (rs_apply.hpp tail_lane)
+  // set by launch_apply: nonzero when the vector kernel also computes the ragged tail S % 16
+  // (no separate byte-kernel launch): (tile << 2) | (last wave << 1) | 1, the tile of each
+  // stripe and the wave (0 or the block's last) that take it (rs_apply.hpp tail_lane)
   uint32_t tail_in_vec;
 };
 
