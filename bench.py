@@ -65,11 +65,15 @@ def parse_args(argv=None):
                    help="configs[3] mode: objects of this size (e.g. 1073741824) split by byte "
                         "columns across the ranks (strong scaling); --stripes objects in total")
     p.add_argument("--erase", default="0,1,2,3", help="erased shard indices for decode")
-    p.add_argument("--split-layout", action="store_true",
-                   help="upstream Split layout (codec.go:31): each object's n shards "
-                        "contiguous at pitch = S, objects back to back (configs[1]: "
-                        "--shard-bytes 6710887, misaligned shards at odd S) instead of the "
-                        "256-B shard pitch")
+    p.add_argument("--split-layout", nargs="?", const="split", default=None,
+                   choices=("split", "readall"),
+                   help="upstream Split layout (codec.go:31) instead of the 256-B shard "
+                        "pitch (configs[1]: --shard-bytes 6710887, misaligned shards at odd "
+                        "S). 'split' (the bare flag): each object's n shards contiguous at "
+                        "pitch = S, objects back to back (a body whose capacity holds all n "
+                        "shards); 'readall': the data shards at pitch = S in page-aligned "
+                        "bodies, the parity in reedsolomon's 64-B AllocAligned buffers (a "
+                        "body from io.ReadAll, as CallFS passes it; device.StripeBatch)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="CPU baseline time budget (0 disables)")
     p.add_argument("--cpu-working-set", type=int, default=2 << 30,
@@ -137,9 +141,9 @@ def cpu_baseline(sb, k, m, erase, seconds, ws_bytes, threads, all_threads=0):
     from oracle import cref
 
     S, n = sb.S, sb.n
-    stripe_bytes = n * sb.pitch
+    stripe_bytes = n * S
     ns = max(1, min(sb.batch, -(-ws_bytes // stripe_bytes)))
-    host = sb.buf[:ns].cpu().numpy()  # GPU-encoded + GPU-decoded stripes, [ns][n][pitch]
+    host = sb.gather(ns).cpu().numpy()  # GPU-encoded + GPU-decoded stripes, [ns][n][S]
     present = [i not in erase for i in range(k + m)]
 
     # bit-exact checks on all ns stripes
@@ -319,7 +323,7 @@ def main(argv=None):
     erase = sorted({int(x) for x in args.erase.split(",") if x != ""})
     present = [i not in erase for i in range(k + m)]
 
-    sb = StripeBatch(k, m, S, B, dev, layout="split" if args.split_layout else "pitch")
+    sb = StripeBatch(k, m, S, B, dev, layout=args.split_layout or "pitch")
     sb.fill_random(0xCA11F5 + rank)
     enc = Plan.for_batch(sb)
     dec = Plan.for_batch(sb, present=present)
@@ -327,11 +331,11 @@ def main(argv=None):
 
     # untimed device-side round-trip check: encode, erase, decode, compare
     enc.launch(stream)
-    ref = sb.buf[:, :, :S].clone()
+    ref = sb.gather()
     for i in erase:
-        sb.buf[:, i, :S].zero_()
+        sb.zero_shard(i)
     dec.launch(stream)
-    if dec.corrupt(stream) or not torch.equal(sb.buf[:, :, :S], ref):
+    if dec.corrupt(stream) or not torch.equal(sb.gather(), ref):
         raise SystemExit("device round trip failed")
     del ref
 
@@ -384,7 +388,7 @@ def main(argv=None):
     ceil = plan_ceilings(enc, dec, stream) if args.ceiling else None
     cfg = {"k": k, "m": m, "shard_bytes": S, "stripes": B}
     if args.split_layout:
-        cfg["layout"] = "split"
+        cfg["layout"] = args.split_layout
     traffic, dec_traffic, tsrc = load_traffic(args.traffic, {**cfg, "erase": erase})
     achieved = enc.bytes / (enc_ms * 1e-3) / 1e9
     dec_achieved = dec.bytes / (dec_ms * 1e-3) / 1e9
@@ -406,8 +410,10 @@ def main(argv=None):
             "workload": (f"RS({k},{m}) device-resident encode + decode(erase {erase}), "
                          + (f"{B} objects of {args.object_bytes} B split by byte columns over "
                             f"{world} GPU(s)" if S_obj else f"{S} B shards, {B} stripes per GPU")
-                         + (", upstream Split layout (pitch = S, contiguous objects)"
-                            if args.split_layout else "")),
+                         + ({"split": ", upstream Split layout (pitch = S, contiguous objects)",
+                             "readall": ", upstream Split layout of an io.ReadAll body (data "
+                                        "shards at pitch = S in the body, parity in 64-B "
+                                        "AllocAligned buffers)"}.get(args.split_layout, ""))),
             **cfg,
             "erase": erase,
             # decode re-verifies only the present parity beyond the first k (a9): none

@@ -28,31 +28,77 @@ class StripeBatch:
     """`batch` stripes of RS(k, m) with shard size S, resident on `device`.
 
     layout "pitch" (default): shards at a 256-B pitch, every shard 16-B aligned.
-    layout "split": upstream `Split`'s layout of contiguous objects (codec.go:31):
-    pitch = S, object b's shard i at b*n*S + i*S, so at odd S every shard but the
-    first sits at its own byte offset (the realigning kernel's case)."""
+    layout "split": upstream `Split`'s layout of contiguous objects (codec.go:31) when the
+    body's capacity holds all n shards: pitch = S, object b's shard i at b*n*S + i*S, so
+    at odd S every shard but the first sits at its own byte offset (the realigning
+    kernel's case).
+    layout "readall": upstream `Split` of a body whose capacity holds the k data shards
+    but not the parity, which is what CallFS passes it: io.ReadAll's body
+    (post_file_enhanced.go:127) grows by append, so cap/len stays below n/k for every
+    profile with m/k > 1/4. The data shards are slices of the body at pitch S (body
+    bases `BODY_ALIGN`-aligned, as the Go heap's large objects are page-aligned); the m
+    parity shards come from reedsolomon's AllocAligned: 64-B aligned, each at a pitch of
+    S rounded up to 64 B (klauspost/reedsolomon v1.13.3 reedsolomon.go Split,
+    galois.go AllocAligned)."""
+
+    BODY_ALIGN = 8192
 
     def __init__(self, k: int, m: int, S: int, batch: int, device: torch.device,
                  layout: str = "pitch"):
-        if layout not in ("pitch", "split"):
+        if layout not in ("pitch", "split", "readall"):
             raise ValueError(f"layout {layout!r}")
         self.k, self.m, self.S, self.batch = k, m, S, batch
         self.n = k + m
         self.layout = layout
-        self.pitch = pitch_for(S) if layout == "pitch" else S
         self.device = torch.device(device)
+        if layout == "readall":
+            self.pitch = S
+            self.body_pitch = -(-k * S // self.BODY_ALIGN) * self.BODY_ALIGN
+            self.par_pitch = -(-S // 64) * 64
+            self.body = torch.empty((batch, self.body_pitch), dtype=torch.uint8, device=self.device)
+            self.par = torch.empty((batch, m, self.par_pitch), dtype=torch.uint8, device=self.device)
+            self.buf = None
+            return
+        self.pitch = pitch_for(S) if layout == "pitch" else S
         self.buf = torch.empty((batch, self.n, self.pitch), dtype=torch.uint8, device=self.device)
 
     def shard(self, b: int, i: int) -> torch.Tensor:
+        if self.buf is None:
+            if i < self.k:
+                return self.body[b, i * self.S:(i + 1) * self.S]
+            return self.par[b, i - self.k, : self.S]
         return self.buf[b, i, : self.S]
 
     def data(self) -> torch.Tensor:
+        if self.buf is None:
+            return self.body[:, : self.k * self.S].view(self.batch, self.k, self.S)
         return self.buf[:, : self.k, : self.S]
 
     def parity(self) -> torch.Tensor:
+        if self.buf is None:
+            return self.par[:, :, : self.S]
         return self.buf[:, self.k:, : self.S]
 
+    def gather(self, stripes: Optional[int] = None) -> torch.Tensor:
+        """A [stripes][n][S] copy of the first `stripes` stripes' shards (all by default)."""
+        ns = self.batch if stripes is None else stripes
+        if self.buf is None:
+            return torch.cat([self.data()[:ns], self.parity()[:ns]], dim=1)
+        return self.buf[:ns, :, : self.S].clone()
+
+    def zero_shard(self, i: int) -> None:
+        """Zero shard i of every stripe."""
+        if self.buf is None:
+            (self.data()[:, i] if i < self.k else self.parity()[:, i - self.k]).zero_()
+        else:
+            self.buf[:, i, : self.S].zero_()
+
     def pointers(self) -> list:
+        if self.buf is None:
+            body, par = self.body.data_ptr(), self.par.data_ptr()
+            return [body + b * self.body_pitch + i * self.S if i < self.k
+                    else par + (b * self.m + i - self.k) * self.par_pitch
+                    for b in range(self.batch) for i in range(self.n)]
         base = self.buf.data_ptr()
         return [base + (b * self.n + i) * self.pitch for b in range(self.batch)
                 for i in range(self.n)]
@@ -60,7 +106,8 @@ class StripeBatch:
     def fill_random(self, seed: int) -> None:
         g = torch.Generator(device=self.device)
         g.manual_seed(seed)
-        self.buf.random_(0, 256, generator=g)
+        for t in ((self.buf,) if self.buf is not None else (self.body, self.par)):
+            t.random_(0, 256, generator=g)
 
 
 class Plan:

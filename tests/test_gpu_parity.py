@@ -1556,6 +1556,48 @@ def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m,
         assert np.array_equal(host[batch - 1, k + j], want[j]), j
 
 
+@pytest.mark.parametrize("k,m,S,batch", [
+    (10, 4, 100_003, 3),       # odd S: every data shard at its own offset, parity 64-B aligned
+    (4, 2, 65_537, 5),
+    (6, 3, 16 * 496 + 16 * 62 + 5, 4),  # realigning kernel's tile / wave edges
+    (12, 4, 5_592_406 // 64, 2),        # even S
+    (10, 4, 1 << 16, 3),                # 16 | S: every shard aligned
+])
+@pytest.mark.parametrize("how", ["rule", "tune"])
+def test_readall_layout_round_trip(native_lib, k, m, S, batch, how):
+    """Upstream Split of an io.ReadAll body (StripeBatch layout "readall": data shards at
+    pitch S inside the body, parity in 64-B AllocAligned buffers at a 64-B pitch): encode
+    against the oracle on every stripe, then a decode of m erasures and one with Verify
+    rows restores every byte; with how="tune" every plan first times each order its
+    kernels offer (misaligned inputs with aligned outputs)."""
+    import torch
+    from callfs_amd.device import Plan, StripeBatch
+    sb = StripeBatch(k, m, S, batch, torch.device("cuda:0"), layout="readall")
+    sb.fill_random(S + 3 * k)
+    ptrs = sb.pointers()
+    assert all(p % 64 == 0 for b in range(batch) for p in ptrs[b * (k + m) + k:(b + 1) * (k + m)])
+
+    def ready(plan):
+        if how == "tune":
+            plan.tune(reps=1)
+        return plan
+
+    ready(Plan.for_batch(sb)).launch()
+    torch.cuda.synchronize()
+    host = sb.gather().cpu().numpy()
+    for b in range(batch):
+        want = cref.encode([host[b, i] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(host[b, k + j], want[j]), (b, j)
+    for erase in (list(range(0, k, max(1, k // m)))[:m], [1, k]):
+        for i in erase:
+            sb.zero_shard(i)
+        dec = ready(Plan.for_batch(sb, present=[i not in erase for i in range(k + m)]))
+        dec.launch()
+        assert not dec.corrupt(), erase
+        assert np.array_equal(sb.gather().cpu().numpy(), host), erase
+
+
 @pytest.mark.parametrize("k,m,L", [(10, 4, 10 * 1000 + 7), (4, 2, 4 * 37 + 1), (16, 4, 4096)])
 def test_small_path_verify_masks_the_tail_vector(codec, k, m, L):
     """Small calls take the one-dispatch path, whose last 16-B vector per shard runs past S

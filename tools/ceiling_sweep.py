@@ -10,7 +10,9 @@ shape spec: k,m,S,stripes[,erase[,layout]]   erase: '-' = encode, 'none' = all p
             or '+'-joined indices (5, 0+3+7+12); layout: 'pitch' (StripeBatch, 256-B
             pitch, default), 'split' (upstream Split layout: object b's shard i at
             base + (b*n + i)*S from an odd base, every shard at its own byte offset when
-            S is odd) or 'contig' (the same from an aligned base)
+            S is odd), 'contig' (the same from an aligned base) or 'readall' (Split of an
+            io.ReadAll body: data shards at pitch S in page-aligned bodies, parity in
+            64-B AllocAligned buffers; device.StripeBatch)
 usage: python tools/ceiling_sweep.py --shape 10,4,1048576,256,5 --shape ... [--tune 1]
 """
 import argparse
@@ -55,7 +57,7 @@ def build(k, m, S, B, layout, dev):
         base = buf.data_ptr() + (1 if layout == "split" else 0)
         ptrs = [base + (b * n + i) * S for b in range(B) for i in range(n)]
         return buf, ptrs
-    sb = StripeBatch(k, m, S, B, dev)
+    sb = StripeBatch(k, m, S, B, dev, layout="readall" if layout == "readall" else "pitch")
     sb.fill_random(0xCA11F5)
     return sb, sb.pointers()
 
