@@ -131,7 +131,9 @@ struct Policy {
   // parity stores both aligned (62 vectors per wave, edge bytes in the first tile)
   static constexpr int REALIGN = REALIGN_;
   // 16-B vectors per tile: REALIGN waves produce 63 vectors from 64 aligned loads
-  static constexpr int WAVE_VECS = REALIGN_ == 2 ? 62 : (REALIGN_ || PROBE_ == 1) ? 63 : 64;
+  // (5: misaligned inputs, aligned outputs, 64 vectors per wave: lane 63 loads its
+  // neighbour vector itself)
+  static constexpr int WAVE_VECS = REALIGN_ == 2 ? 62 : ((REALIGN_ && REALIGN_ != 5) || PROBE_ == 1) ? 63 : 64;
   static constexpr int TILE_VECS = WAVE_VECS < 64 ? BS_ / 64 * WAVE_VECS : BS_ * U_;
   static constexpr int WPE = WPE_;
   static constexpr int U = U_;
@@ -439,6 +441,27 @@ __device__ __forceinline__ uint4 shift_from_next_sel(const uint4& A, uint32_t d)
 }
 __device__ __forceinline__ uint4 realign_sel(const uint8_t* p, const uint4& A) {
   return shift_from_next_sel(A, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 15u);
+}
+
+// REALIGN 5 (outputs 16-B aligned): waves of 64 vectors, so every wave's stores fill
+// whole 1 KiB windows of the output rows. Lane 63's A[v+1] is the first vector of the
+// next wave's window: lane 63 alone loads it (one single-lane load per shard, E below) and
+// the DPP that hands every other lane its neighbour's A leaves E in lane 63 (bound_ctrl
+// off: a lane whose source is out of the wave keeps the `old` operand).
+__device__ __forceinline__ uint4 shift_from_next_e(const uint4& A, const uint4& E, uint32_t d) {
+  if (d == 0) return A;  // wave-uniform
+  auto nx = [](uint32_t v, uint32_t old) {
+    return static_cast<uint32_t>(
+        __builtin_amdgcn_update_dpp(static_cast<int>(old), static_cast<int>(v), 0x130, 0xf, 0xf, false));
+  };
+  const uint4 B = make_uint4(nx(A.x, E.x), nx(A.y, E.y), nx(A.z, E.z), nx(A.w, E.w));
+  const uint32_t r = d & 3u;
+  switch (d >> 2) {  // wave-uniform
+    case 0: return funnel16<0>(A, B, r);
+    case 1: return funnel16<1>(A, B, r);
+    case 2: return funnel16<2>(A, B, r);
+    default: return funnel16<3>(A, B, r);
+  }
 }
 
 // ---- aligned parity stores of misaligned rows (Policy::REALIGN == 2) -----------------
@@ -829,7 +852,32 @@ void rs_apply_lds(ApplyArgs a) {
     if constexpr (P::REALIGN) {
       static_assert(!P::NOMATH, "REALIGN: no NOMATH form");
       auto lda = [&](int i) { return ld_aligned<P>(in[i], v0, a.nvec); };
-      if constexpr (P::WIX == 2) {
+      if constexpr (P::REALIGN == 5) {
+        // ring of three (aligned vector, lane 63's extra) pairs, realigned when consumed
+        auto lde = [&](int i) {
+          uint4 e = make_uint4(0, 0, 0, 0);
+          if (lane == 63u) e = ld_aligned<P>(in[i], v0 + 1, a.nvec);
+          return e;
+        };
+        uint4 x0 = lda(0), e0 = lde(0), x1 = x0, e1 = e0, x2 = x0, e2 = e0;
+        if (K > 1) {
+          x1 = lda(1);
+          e1 = lde(1);
+        }
+#pragma unroll 1
+        for (int i = 0; i < K; ++i) {
+          if (i + 2 < K) {
+            x2 = lda(i + 2);
+            e2 = lde(i + 2);
+          }
+          lds_mac<RT>(acc, shift_from_next_e(x0, e0, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(in[i])) & 15u),
+                      lds0 + static_cast<uint32_t>(i) * 32u * W);
+          x0 = x1;
+          e0 = e1;
+          x1 = x2;
+          e1 = e2;
+        }
+      } else if constexpr (P::WIX == 2) {
         // triples of aligned loads (as the aligned triple loop below): the next triple's
         // three loads in flight while one is realigned and looked up
         const int KT = K / 3;

@@ -101,6 +101,13 @@ using LdsTriVerifyPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, 
 template <int R, int ORD>
 using LdsRealignTriPolicy =
     dev::Policy<(R <= 4 ? 7 : 2), 1, true, true, false, 512, 2, ORD, 0, false, 2, false, 0, 0, 2>;
+// Misaligned inputs with 16-B-aligned outputs (upstream Split of an io.ReadAll body: the
+// data shards inside the body, the parity in reedsolomon's AllocAligned buffers): 64-vector
+// waves, lane 63's neighbour vector from one single-lane load per shard (rs_apply.hpp
+// REALIGN 5), so the parity stores fill whole 1 KiB windows
+template <int R, int ORD>
+using LdsRealign64Policy =
+    dev::Policy<6, 1, true, true, false, 512, 2, ORD, 0, false, 5>;
 template <int ORD>
 using LdsRealignOutPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 2>;
 template <int ORD>
@@ -330,6 +337,15 @@ const std::array<std::array<VecFn, 8>, 3> kLdsRealignTri = {
     lds_realign_tri_table<10>(std::make_integer_sequence<int, 8>{}),
     lds_realign_tri_table<11>(std::make_integer_sequence<int, 8>{})};
 template <int ORD, int... Rs>
+constexpr auto lds_realign64_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealign64Policy<Rs + 1, ORD>>...};
+}
+// [consecutive, X8, X32][R - 1]
+const std::array<std::array<VecFn, 8>, 3> kLdsRealign64 = {
+    lds_realign64_table<0>(std::make_integer_sequence<int, 8>{}),
+    lds_realign64_table<10>(std::make_integer_sequence<int, 8>{}),
+    lds_realign64_table<11>(std::make_integer_sequence<int, 8>{})};
+template <int ORD, int... Rs>
 constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1, ORD>>...};
 }
@@ -452,10 +468,27 @@ bool wix_enabled() {
 // The rule's triple-form order (tile_order.hpp tri_rule_order: round 4 adds X32 for K <= 4,
 // X32 / Q16 for K 5..6 and Q16 on 16-32 MiB power-of-two pitches), or -1. With
 // CALLFS_RS_TILE_ORDER set, the triple form follows the forced order with round 3's bounds.
+// Misaligned inputs with 16-B-aligned outputs (upstream Split of an io.ReadAll body: the
+// data shards inside the body, the parity in AllocAligned buffers): the triple form with
+// unaligned 16-B loads, X32 up to 256 tiles per stripe and X8 above, not the realigning
+// kernel. tools/unaligned_tri_probe.sh (profiles/r04/utri1/readall_enc.jsonl, % of 8 TB/s,
+// realigning kernel (rule) -> triples in X32 / X8): RS(10,4) 104,858 B 69.5 -> 76.7 (G2
+// 77.5), RS(12,4) 87,382 B 69.0 -> 75.7, RS(5,3) 209,716 B 71.0 -> 78.3, RS(6,3) 174,763 B
+// 70.6 -> 74.4, RS(10,8) 1,048,577 B 68.8 -> 70.9, RS(10,4) 6,710,887 B 71.2 -> 72.8 (X8),
+// RS(12,4) 5,592,406 B 71.8 -> 74.2 (X8), RS(4,2) 1,048,577 B 71.0 -> 71.9. With unaligned
+// stores as well (the contiguous Split layout) the same forms lost 1-6 points
+// (split_enc.jsonl), so misaligned outputs keep the realigning kernel.
+int tri_unaligned_order(const ApplyArgs& a, uint64_t tps) {
+  if (a.R > 8 || a.K < 4 || !a.in_misalign || a.out_misalign || tile_order_override() >= 0)
+    return -1;
+  return static_cast<int>(tps <= 256 ? TileOrder::kXcd32 : TileOrder::kXcd8);
+}
+
 int tri_rule_of(const ApplyArgs& a) {
   if (!wix_enabled() || !takes_lds(a)) return -1;
   const uint32_t rows = (1u << a.R) - 1;
   const uint64_t tps = (a.nvec + LdsPolicy::BS - 1) / LdsPolicy::BS;
+  if (a.in_misalign && !a.out_misalign) return tri_unaligned_order(a, tps);
   const bool mis = (a.in_misalign | a.out_misalign) != 0, verify = (a.verify_mask & rows) != 0,
              read_only = (a.verify_mask & rows) == rows;
   if (tile_order_override() >= 0)
@@ -483,7 +516,11 @@ int tri_index(TileOrder o) {
   }
 }
 bool takes_realign(const ApplyArgs& a) {
-  return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u);
+  return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u) && !takes_tri(a);
+}
+// the 64-vector realigning form: misaligned inputs, every output 16-B aligned
+bool can_realign64(const ApplyArgs& a) {
+  return can_realign(a) && a.in_misalign && !a.out_misalign;
 }
 
 // The rule's realigning launches with triple loads (tile_order.hpp realign_tri_rule);
@@ -531,6 +568,9 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
     const auto rtri_in = [](TileOrder o) {
       return static_cast<TileOrder>(kOrderRealignTri + static_cast<int>(o));
     };
+    const auto r64_in = [](TileOrder o) {
+      return static_cast<TileOrder>(kOrderRealign64 + static_cast<int>(o));
+    };
     const auto wix_in = [](TileOrder o) {
       return static_cast<TileOrder>(kOrderWix + static_cast<int>(o));
     };
@@ -548,6 +588,11 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(realign_in(TileOrder::kXcd32));
       add(realign_in(TileOrder::kConsecutive));
       if (every_instance) add(realign_in(TileOrder::kXcd8));
+      if (can_realign64(a)) {
+        add(r64_in(TileOrder::kXcd32));
+        add(r64_in(TileOrder::kConsecutive));
+        if (every_instance) add(r64_in(TileOrder::kXcd8));
+      }
       if (a.K >= 3) {  // the realigning kernel with triple loads
         add(rtri_in(TileOrder::kXcd32));
         add(rtri_in(TileOrder::kConsecutive));
@@ -567,7 +612,12 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(TileOrder::kXcd8);
       add(TileOrder::kXcd32);
     }
-    if ((every_instance && a.K >= 3 && !(a.in_misalign | a.out_misalign)) || tri_tunable_launch(a)) {
+    // (on misaligned shards the triple forms are the plain kernel's unaligned 16-B
+    // accesses: A/B instances for rs_plan_set_orders)
+    // (misaligned launches: the tuner also times the triple forms' unaligned accesses,
+    // which the rule takes for aligned outputs only)
+    if ((every_instance && a.K >= 3) || tri_tunable_launch(a) ||
+        (a.in_misalign && a.R <= 8 && a.K >= 4 && wix_enabled())) {
       add(tri_in(TileOrder::kConsecutive));
       add(tri_in(TileOrder::kGroup2));
       add(tri_in(TileOrder::kXcd32));
@@ -597,6 +647,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
   // realigning kernel with triple loads: kOrderRealignTri + its order -> kOrderRealign + it
+  const bool r64 = order >= kOrderRealign64 && can_realign64(a);
+  if (order >= kOrderRealign64) order = r64 ? order - kOrderRealign64 + kOrderRealign : -1;
   const bool rtri = order >= kOrderRealignTri && a.K >= 3 && can_realign(a);
   if (order >= kOrderRealignTri) order = rtri ? order - kOrderRealignTri + kOrderRealign : -1;
   bool tri = order >= kOrderTri && a.R <= 8 && a.K >= 3;
@@ -671,7 +723,12 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
                       "one grid shape for every LDS policy");
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         // misaligned shards: the realigning form, unless a tuned order names a plain kernel
-        if (can_realign(a) && (order >= kOrderRealign || (order < 0 && takes_realign(a)))) {
+        if (r64) {  // 512-vector tiles and the ragged tail as the plain kernel's
+          static_assert(LdsRealign64Policy<1, 0>::TILE_VECS == LdsPolicy::TILE_VECS &&
+                            LdsRealign64Policy<8, 0>::TILE_VECS == LdsPolicy::TILE_VECS,
+                        "REALIGN 5 tiles as the plain kernel's");
+          fn = kLdsRealign64[realign_order_index(order)][a.R - 1];
+        } else if (can_realign(a) && (order >= kOrderRealign || (order < 0 && takes_realign(a)))) {
           fn = (rtri || (order < 0 && takes_realign_tri(a)) ? kLdsRealignTri : kLdsRealignOut)
               [realign_order_index(order)][a.R - 1];
           gx = dev::vec_grid<LdsRealignOutPolicy<0>>(a.nvec, a.batch);
@@ -770,7 +827,8 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
   a.tail_in_vec = a.nvec * 16 < a.S ? tail_code(a.nvec, LdsPolicy::TILE_VECS, LdsPolicy::BS) : 0u;
-  if (order >= kOrderRealignTri) order = order - kOrderRealignTri + kOrderRealign;
+  if (order >= kOrderRealign64) order = order - kOrderRealign64 + kOrderRealign;
+  else if (order >= kOrderRealignTri) order = order - kOrderRealignTri + kOrderRealign;
   else if (order >= kOrderTri) order -= kOrderTri;
   if (order >= kOrderWix) order -= kOrderWix;  // bounded by the nibble kernel's traffic
   // the order the production launch would take (a tuned order, else the rule; the

@@ -114,6 +114,12 @@ constexpr int kOrderTri = 96;
 // (kOrderRealignTri + consecutive / X8 / X32: the realigning kernel with its aligned loads
 // issued in triples)
 constexpr int kOrderRealignTri = 128;
+// (kOrderRealign64 + consecutive / X8 / X32: misaligned inputs with 16-B-aligned outputs --
+// upstream Split of an io.ReadAll body, whose parity reedsolomon allocates aligned -- in
+// 64-vector waves: aligned loads realigned in registers, lane 63's neighbour vector from
+// one extra single-lane load, stores unshifted in 1 KiB wave windows; rs_apply.hpp
+// REALIGN 5)
+constexpr int kOrderRealign64 = 160;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the

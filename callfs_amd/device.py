@@ -24,6 +24,16 @@ def pitch_for(S: int) -> int:
     return (S + 255) // 256 * 256
 
 
+def _aligned_empty(shape, align: int, device) -> torch.Tensor:
+    """An uninitialised uint8 tensor of `shape` whose first byte is `align`-aligned."""
+    n = 1
+    for d in shape:
+        n *= d
+    raw = torch.empty(n + align, dtype=torch.uint8, device=device)
+    off = -raw.data_ptr() % align
+    return raw[off:off + n].view(shape)
+
+
 class StripeBatch:
     """`batch` stripes of RS(k, m) with shard size S, resident on `device`.
 
@@ -32,6 +42,9 @@ class StripeBatch:
     body's capacity holds all n shards: pitch = S, object b's shard i at b*n*S + i*S, so
     at odd S every shard but the first sits at its own byte offset (the realigning
     kernel's case).
+    layout "planar": the pitch layout's 256-B shard pitch, but the k data shards of every
+    stripe in one region ([batch][k][pitch]) and the m parity shards in another
+    ([batch][m][pitch]), so no stripe's parity sits between two stripes' data.
     layout "readall": upstream `Split` of a body whose capacity holds the k data shards
     but not the parity, which is what CallFS passes it: io.ReadAll's body
     (post_file_enhanced.go:127) grows by append, so cap/len stays below n/k for every
@@ -45,18 +58,24 @@ class StripeBatch:
 
     def __init__(self, k: int, m: int, S: int, batch: int, device: torch.device,
                  layout: str = "pitch"):
-        if layout not in ("pitch", "split", "readall"):
+        if layout not in ("pitch", "split", "readall", "planar"):
             raise ValueError(f"layout {layout!r}")
         self.k, self.m, self.S, self.batch = k, m, S, batch
         self.n = k + m
         self.layout = layout
         self.device = torch.device(device)
-        if layout == "readall":
-            self.pitch = S
-            self.body_pitch = -(-k * S // self.BODY_ALIGN) * self.BODY_ALIGN
-            self.par_pitch = -(-S // 64) * 64
-            self.body = torch.empty((batch, self.body_pitch), dtype=torch.uint8, device=self.device)
-            self.par = torch.empty((batch, m, self.par_pitch), dtype=torch.uint8, device=self.device)
+        if layout in ("readall", "planar"):
+            # data shard i of stripe b at body + b*body_pitch + i*pitch, parity j at
+            # par + (b*m + j)*par_pitch
+            if layout == "readall":
+                self.pitch = S
+                self.body_pitch = -(-k * S // self.BODY_ALIGN) * self.BODY_ALIGN
+                self.par_pitch = -(-S // 64) * 64
+            else:
+                self.pitch = self.par_pitch = pitch_for(S)
+                self.body_pitch = k * self.pitch
+            self.body = _aligned_empty((batch, self.body_pitch), self.BODY_ALIGN, self.device)
+            self.par = _aligned_empty((batch, m, self.par_pitch), 256, self.device)
             self.buf = None
             return
         self.pitch = pitch_for(S) if layout == "pitch" else S
@@ -65,13 +84,13 @@ class StripeBatch:
     def shard(self, b: int, i: int) -> torch.Tensor:
         if self.buf is None:
             if i < self.k:
-                return self.body[b, i * self.S:(i + 1) * self.S]
+                return self.body[b, i * self.pitch:i * self.pitch + self.S]
             return self.par[b, i - self.k, : self.S]
         return self.buf[b, i, : self.S]
 
     def data(self) -> torch.Tensor:
         if self.buf is None:
-            return self.body[:, : self.k * self.S].view(self.batch, self.k, self.S)
+            return self.body[:, : self.k * self.pitch].view(self.batch, self.k, self.pitch)[:, :, : self.S]
         return self.buf[:, : self.k, : self.S]
 
     def parity(self) -> torch.Tensor:
@@ -96,7 +115,7 @@ class StripeBatch:
     def pointers(self) -> list:
         if self.buf is None:
             body, par = self.body.data_ptr(), self.par.data_ptr()
-            return [body + b * self.body_pitch + i * self.S if i < self.k
+            return [body + b * self.body_pitch + i * self.pitch if i < self.k
                     else par + (b * self.m + i - self.k) * self.par_pitch
                     for b in range(self.batch) for i in range(self.n)]
         base = self.buf.data_ptr()
@@ -190,7 +209,8 @@ class Plan:
                    64: "wix", 65: "wix-g8", 66: "wix-g2", 67: "wix-q8", 68: "wix-q16",
                    69: "wix-x8", 70: "wix-x32", 96: "tri", 98: "tri-g2", 99: "tri-q8",
                    100: "tri-q16", 101: "tri-x8", 102: "tri-x32", 128: "realign-tri", 133: "realign-tri-x8",
-                   134: "realign-tri-x32"}
+                   134: "realign-tri-x32", 160: "realign64", 165: "realign64-x8",
+                   166: "realign64-x32"}
 
     def tune(self, reps: int = 5, stream: Optional[torch.cuda.Stream] = None) -> list:
         """rs_plan_tune: time each launch group in every tile order its kernel offers

@@ -1563,23 +1563,31 @@ def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m,
     (12, 4, 5_592_406 // 64, 2),        # even S
     (10, 4, 1 << 16, 3),                # 16 | S: every shard aligned
 ])
-@pytest.mark.parametrize("how", ["rule", "tune"])
+@pytest.mark.parametrize("how", ["rule", "tune", "realign64-x32", "realign64", "realign64-x8",
+                                 "tri-x32", "tri-g2"])
 def test_readall_layout_round_trip(native_lib, k, m, S, batch, how):
     """Upstream Split of an io.ReadAll body (StripeBatch layout "readall": data shards at
     pitch S inside the body, parity in 64-B AllocAligned buffers at a 64-B pitch): encode
-    against the oracle on every stripe, then a decode of m erasures and one with Verify
-    rows restores every byte; with how="tune" every plan first times each order its
-    kernels offer (misaligned inputs with aligned outputs)."""
+    against the oracle on every stripe, then decodes of m data erasures, of erasures with
+    Verify rows and of the parity alone restore every byte. how="tune": every plan first
+    times each order its kernels offer; otherwise every plan is pinned to that kernel form
+    (rs_plan_set_orders) where its launch offers it: the 64-vector realigning form
+    (REALIGN 5, misaligned inputs with aligned outputs: the encode and the parity-only
+    decode) or the triple loop's unaligned accesses."""
     import torch
+    from callfs_amd import _native as N
     from callfs_amd.device import Plan, StripeBatch
     sb = StripeBatch(k, m, S, batch, torch.device("cuda:0"), layout="readall")
     sb.fill_random(S + 3 * k)
     ptrs = sb.pointers()
     assert all(p % 64 == 0 for b in range(batch) for p in ptrs[b * (k + m) + k:(b + 1) * (k + m)])
+    aligned = S % 16 == 0  # every data shard 16-B aligned: no realigning form
 
-    def ready(plan):
+    def ready(plan, outputs_aligned=True):
         if how == "tune":
             plan.tune(reps=1)
+        elif how != "rule" and not (how.startswith("realign64") and (aligned or not outputs_aligned)):
+            plan.set_orders([how] * int(N.lib.rs_plan_groups(plan.handle)))
         return plan
 
     ready(Plan.for_batch(sb)).launch()
@@ -1589,10 +1597,11 @@ def test_readall_layout_round_trip(native_lib, k, m, S, batch, how):
         want = cref.encode([host[b, i] for i in range(k)], k, m)
         for j in range(m):
             assert np.array_equal(host[b, k + j], want[j]), (b, j)
-    for erase in (list(range(0, k, max(1, k // m)))[:m], [1, k]):
+    for erase in (list(range(0, k, max(1, k // m)))[:m], [1, k], list(range(k, k + m))):
         for i in erase:
             sb.zero_shard(i)
-        dec = ready(Plan.for_batch(sb, present=[i not in erase for i in range(k + m)]))
+        dec = ready(Plan.for_batch(sb, present=[i not in erase for i in range(k + m)]),
+                    outputs_aligned=min(erase) >= k)
         dec.launch()
         assert not dec.corrupt(), erase
         assert np.array_equal(sb.gather().cpu().numpy(), host), erase
