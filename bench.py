@@ -65,6 +65,14 @@ def parse_args(argv=None):
                    help="configs[3] mode: objects of this size (e.g. 1073741824) split by byte "
                         "columns across the ranks (strong scaling); --stripes objects in total")
     p.add_argument("--erase", default="0,1,2,3", help="erased shard indices for decode")
+    p.add_argument("--layout", default="planar", choices=("planar", "pitch", "split", "readall"),
+                   help="shard layout in HBM (device.StripeBatch): 'planar' (default since round "
+                        "4: 256-B shard pitch, every stripe's data shards in one region and its "
+                        "parity in another), 'pitch' (the same pitch, each stripe's n shards in one "
+                        "block: rounds 1-3), or an upstream Split layout (--split-layout)")
+    p.add_argument("--layout-ab", type=int, default=1,
+                   help="1: with --layout planar, also time the same workload's kernels in the "
+                        "'pitch' layout in this process (tuned as well): line['layout_ab']")
     p.add_argument("--split-layout", nargs="?", const="split", default=None,
                    choices=("split", "readall"),
                    help="upstream Split layout (codec.go:31) instead of the 256-B shard "
@@ -251,6 +259,34 @@ def plan_ceilings(enc, dec, stream):
     return out
 
 
+def layout_ab(k, m, S, B, dev, present, stream, tune):
+    """The same encode and decode in the 'pitch' layout (256-B shard pitch, each stripe's n
+    shards in one block, the bench layout of rounds 1-3), timed in this process after the
+    bench's own plans: a second batch, its plans tuned as the bench's are, mean kernel time
+    of 20 event-timed launches after >= 30 ms of warmup each (_launch_ms)."""
+    from callfs_amd.device import Plan, StripeBatch
+    sb = StripeBatch(k, m, S, B, dev, layout="pitch")
+    sb.fill_random(0x5EED)
+    enc, dec = Plan.for_batch(sb), Plan.for_batch(sb, present=present)
+    enc.launch(stream)
+    orders = ({"encode": enc.tune(stream=stream), "decode": dec.tune(stream=stream)}
+              if tune else None)
+    out = {"pitch": {"tile_order": orders}}
+    for name, plan in (("encode", enc), ("decode", dec)):
+        ms = _launch_ms(lambda evs: plan.launch(stream, events=evs), stream)
+        out["pitch"][name + "_frac"] = round(plan.bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if dec.corrupt(stream):
+        raise SystemExit("pitch-layout decode flagged corruption")
+    enc.close()
+    dec.close()
+    del sb
+    torch.cuda.empty_cache()
+    out["note"] = ("kernel-time fractions of 8 TB/s, same workload, same process: the bench "
+                   "layout ('planar') against each stripe's data and parity in one block "
+                   "('pitch'); DESIGN.md §4")
+    return out
+
+
 def load_traffic(path, cfg):
     """PMC-measured HBM bytes per encode / decode launch for this exact config."""
     try:
@@ -323,7 +359,8 @@ def main(argv=None):
     erase = sorted({int(x) for x in args.erase.split(",") if x != ""})
     present = [i not in erase for i in range(k + m)]
 
-    sb = StripeBatch(k, m, S, B, dev, layout=args.split_layout or "pitch")
+    layout = args.split_layout or args.layout
+    sb = StripeBatch(k, m, S, B, dev, layout=layout)
     sb.fill_random(0xCA11F5 + rank)
     enc = Plan.for_batch(sb)
     dec = Plan.for_batch(sb, present=present)
@@ -387,8 +424,8 @@ def main(argv=None):
         raise SystemExit("verify flagged corruption during the timed run")
     ceil = plan_ceilings(enc, dec, stream) if args.ceiling else None
     cfg = {"k": k, "m": m, "shard_bytes": S, "stripes": B}
-    if args.split_layout:
-        cfg["layout"] = args.split_layout
+    if layout != "pitch":
+        cfg["layout"] = layout
     traffic, dec_traffic, tsrc = load_traffic(args.traffic, {**cfg, "erase": erase})
     achieved = enc.bytes / (enc_ms * 1e-3) / 1e9
     dec_achieved = dec.bytes / (dec_ms * 1e-3) / 1e9
@@ -413,7 +450,9 @@ def main(argv=None):
                          + ({"split": ", upstream Split layout (pitch = S, contiguous objects)",
                              "readall": ", upstream Split layout of an io.ReadAll body (data "
                                         "shards at pitch = S in the body, parity in 64-B "
-                                        "AllocAligned buffers)"}.get(args.split_layout, ""))),
+                                        "AllocAligned buffers)",
+                             "planar": ", 256-B shard pitch, data and parity shards in two "
+                                       "regions"}.get(layout, ""))),
             **cfg,
             "erase": erase,
             # decode re-verifies only the present parity beyond the first k (a9): none
@@ -462,6 +501,10 @@ def main(argv=None):
         },
         "cpu_baseline": None,
     }
+    if layout == "planar" and args.layout_ab:
+        line["layout_ab"] = layout_ab(k, m, S, B, dev, present, stream, args.tune)
+        line["layout_ab"]["planar"] = {"encode_frac": line["roofline"]["frac"],
+                                       "decode_frac": line["roofline_decode"]["frac"]}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         visible = len(os.sched_getaffinity(0))
         threads = args.cpu_threads or max(1, min(CPU_SHARE, visible))

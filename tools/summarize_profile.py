@@ -33,7 +33,8 @@ def _per_op(rows, key, steps, slices):
     return enc, dec
 
 
-def main(src, dst, k=10, m=4, S=1 << 20, B=256, erase=(0, 1, 2, 3), kernel="rs_apply"):
+def main(src, dst, k=10, m=4, S=1 << 20, B=256, erase=(0, 1, 2, 3), layout="planar",
+         kernel="rs_apply"):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     algo = B * S * (k + m)
@@ -43,7 +44,8 @@ def main(src, dst, k=10, m=4, S=1 << 20, B=256, erase=(0, 1, 2, 3), kernel="rs_a
     rows = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
     ks = [r for r in rows if r["Name"] == hot_name][0]
     out = {
-        "config": {"k": k, "m": m, "shard_bytes": S, "stripes": B, "erase": list(erase)},
+        "config": {"k": k, "m": m, "shard_bytes": S, "stripes": B,
+                   **({"layout": layout} if layout != "pitch" else {}), "erase": list(erase)},
         "kernel": ks["Name"],
         "kernel_stats": {"calls": int(ks["Calls"]), "avg_ns": float(ks["AverageNs"]),
                          "min_ns": float(ks["MinNs"]), "max_ns": float(ks["MaxNs"])},
@@ -113,4 +115,6 @@ if __name__ == "__main__":
     extra = [int(x) for x in a[2:6]]
     if len(a) > 6:
         extra.append(tuple(int(x) for x in a[6].split(",")))
+    if len(a) > 7:
+        extra.append(a[7])
     main(a[0], a[1], *extra)
