@@ -45,6 +45,8 @@ class StripeBatch:
     layout "planar": the pitch layout's 256-B shard pitch, but the k data shards of every
     stripe in one region ([batch][k][pitch]) and the m parity shards in another
     ([batch][m][pitch]), so no stripe's parity sits between two stripes' data.
+    layout "shardmajor": the 256-B pitch with all stripes' shard i in one region
+    ([n][batch][pitch]).
     layout "readall": upstream `Split` of a body whose capacity holds the k data shards
     but not the parity, which is what CallFS passes it: io.ReadAll's body
     (post_file_enhanced.go:127) grows by append, so cap/len stays below n/k for every
@@ -58,7 +60,7 @@ class StripeBatch:
 
     def __init__(self, k: int, m: int, S: int, batch: int, device: torch.device,
                  layout: str = "pitch"):
-        if layout not in ("pitch", "split", "readall", "planar"):
+        if layout not in ("pitch", "split", "readall", "planar", "shardmajor"):
             raise ValueError(f"layout {layout!r}")
         self.k, self.m, self.S, self.batch = k, m, S, batch
         self.n = k + m
@@ -78,7 +80,11 @@ class StripeBatch:
             self.par = _aligned_empty((batch, m, self.par_pitch), 256, self.device)
             self.buf = None
             return
-        self.pitch = pitch_for(S) if layout == "pitch" else S
+        self.pitch = S if layout == "split" else pitch_for(S)
+        if layout == "shardmajor":
+            sm = torch.empty((self.n, batch, self.pitch), dtype=torch.uint8, device=self.device)
+            self.buf = sm.permute(1, 0, 2)  # [batch][n][pitch] view of [n][batch][pitch]
+            return
         self.buf = torch.empty((batch, self.n, self.pitch), dtype=torch.uint8, device=self.device)
 
     def shard(self, b: int, i: int) -> torch.Tensor:
@@ -119,8 +125,8 @@ class StripeBatch:
                     else par + (b * self.m + i - self.k) * self.par_pitch
                     for b in range(self.batch) for i in range(self.n)]
         base = self.buf.data_ptr()
-        return [base + (b * self.n + i) * self.pitch for b in range(self.batch)
-                for i in range(self.n)]
+        sb_, si_ = self.buf.stride(0), self.buf.stride(1)
+        return [base + b * sb_ + i * si_ for b in range(self.batch) for i in range(self.n)]
 
     def fill_random(self, seed: int) -> None:
         g = torch.Generator(device=self.device)

@@ -8,7 +8,7 @@ import torch
 from callfs_amd.device import StripeBatch
 
 
-@pytest.mark.parametrize("layout", ["pitch", "split", "readall", "planar"])
+@pytest.mark.parametrize("layout", ["pitch", "split", "readall", "planar", "shardmajor"])
 @pytest.mark.parametrize("k,m,S,batch", [(10, 4, 1001, 3), (4, 2, 4096, 2), (6, 3, 17, 5)])
 def test_layout_views_and_pointers_agree(layout, k, m, S, batch):
     sb = StripeBatch(k, m, S, batch, torch.device("cpu"), layout=layout)

@@ -57,7 +57,7 @@ def build(k, m, S, B, layout, dev):
         base = buf.data_ptr() + (1 if layout == "split" else 0)
         ptrs = [base + (b * n + i) * S for b in range(B) for i in range(n)]
         return buf, ptrs
-    sb = StripeBatch(k, m, S, B, dev, layout=layout if layout in ("readall", "planar") else "pitch")
+    sb = StripeBatch(k, m, S, B, dev, layout=layout if layout in ("readall", "planar", "shardmajor") else "pitch")
     sb.fill_random(0xCA11F5)
     return sb, sb.pointers()
 
