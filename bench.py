@@ -70,6 +70,10 @@ def parse_args(argv=None):
                         "4: 256-B shard pitch, every stripe's data shards in one region and its "
                         "parity in another), 'pitch' (the same pitch, each stripe's n shards in one "
                         "block: rounds 1-3), or an upstream Split layout (--split-layout)")
+    p.add_argument("--decode-into", default="fresh", choices=("fresh", "inplace"),
+                   help="with --layout planar: rebuild the erased shards into a region of "
+                        "their own ('fresh', as reedsolomon's Reconstruct allocates missing "
+                        "shards) or into their slots of the batch ('inplace')")
     p.add_argument("--layout-ab", type=int, default=1,
                    help="1: with --layout planar, also time the same workload's kernels in the "
                         "'pitch' layout in this process (tuned as well): line['layout_ab']")
@@ -363,18 +367,43 @@ def main(argv=None):
     sb = StripeBatch(k, m, S, B, dev, layout=layout)
     sb.fill_random(0xCA11F5 + rank)
     enc = Plan.for_batch(sb)
-    dec = Plan.for_batch(sb, present=present)
+    # decode into fresh buffers (layout planar, --decode-into fresh): the erased shards are
+    # rebuilt into their own region, as reedsolomon's Reconstruct allocates the missing
+    # shards of a download (codec.go:55) instead of writing over survivors' neighbours;
+    # otherwise into the erased shards' own slots of the batch
+    fresh = layout == "planar" and args.decode_into == "fresh" and erase
+    rebuilt = None
+    if fresh:
+        from callfs_amd.device import _aligned_empty
+        rebuilt = _aligned_empty((B, len(erase), sb.pitch), 256, dev)
+        ptrs = sb.pointers()
+        for b in range(B):
+            for j, i in enumerate(erase):
+                ptrs[b * (k + m) + i] = rebuilt[b, j].data_ptr()
+        dec = Plan(k, m, S, B, ptrs, present=present, device=local)
+    else:
+        dec = Plan.for_batch(sb, present=present)
     stream = torch.cuda.current_stream(dev)
+
+    def rebuilt_ok():
+        want = sb.gather()[:, erase]
+        return torch.equal(rebuilt[:, :, :S], want)
 
     # untimed device-side round-trip check: encode, erase, decode, compare
     enc.launch(stream)
-    ref = sb.gather()
-    for i in erase:
-        sb.zero_shard(i)
-    dec.launch(stream)
-    if dec.corrupt(stream) or not torch.equal(sb.gather(), ref):
-        raise SystemExit("device round trip failed")
-    del ref
+    if fresh:
+        rebuilt.zero_()
+        dec.launch(stream)
+        if dec.corrupt(stream) or not rebuilt_ok():
+            raise SystemExit("device round trip failed")
+    else:
+        ref = sb.gather()
+        for i in erase:
+            sb.zero_shard(i)
+        dec.launch(stream)
+        if dec.corrupt(stream) or not torch.equal(sb.gather(), ref):
+            raise SystemExit("device round trip failed")
+        del ref
 
     # untimed: pick each plan's tile order on this box (the outputs are recomputed to the
     # same bytes; DESIGN.md §5 "Tile order")
@@ -422,6 +451,11 @@ def main(argv=None):
 
     if dec.corrupt(stream):
         raise SystemExit("verify flagged corruption during the timed run")
+    if fresh:
+        rebuilt.zero_()
+        dec.launch(stream)
+        if not rebuilt_ok():
+            raise SystemExit("rebuilt shards differ from the originals after the timed run")
     ceil = plan_ceilings(enc, dec, stream) if args.ceiling else None
     cfg = {"k": k, "m": m, "shard_bytes": S, "stripes": B}
     if layout != "pitch":
@@ -455,6 +489,7 @@ def main(argv=None):
                                        "regions"}.get(layout, ""))),
             **cfg,
             "erase": erase,
+            "decode_into": "fresh buffers (a region of their own)" if fresh else "the batch",
             # decode re-verifies only the present parity beyond the first k (a9): none
             # when exactly k shards survive, as with the default 4-of-14 erasure
             "decode_verify_rows": verify_rows,
@@ -511,6 +546,11 @@ def main(argv=None):
         line["cpu_baseline"] = cpu_baseline(sb, k, m, erase, args.cpu_seconds,
                                             args.cpu_working_set, threads, all_threads=visible)
         line["cpu_baseline"]["cores_visible"] = visible
+        if fresh:
+            line["cpu_baseline"]["parity_check"] += (
+                "; the decode rebuilds into fresh buffers, checked == the original shards "
+                "on the device after the timed run, and the CPU reconstruction == the "
+                "same originals")
         if threads < visible:
             line["cpu_baseline"]["threads_note"] = (
                 f"{threads} of {visible} visible cores: the GPU box's CPU share per GPU is "
