@@ -114,7 +114,7 @@ struct Policy {
   // (WIX 2 with REALIGN: the realigning kernel's aligned loads issued in triples)
   static constexpr int WIX = WIX_;
   // (WIX 2 with VPF: the aligned triple loop with early compare loads)
-  static_assert(!WIX_ || ((REALIGN_ == 0 || WIX_ == 2) && (VPF_ == 0 || ((WIX_ == 2 || WIX_ == 3) && REALIGN_ == 0)) &&
+  static_assert(!WIX_ || ((REALIGN_ == 0 || WIX_ == 2 || (WIX_ == 3 && REALIGN_ == 2)) && (VPF_ == 0 || ((WIX_ == 2 || WIX_ == 3) && REALIGN_ == 0)) &&
                           RING_ == 0 && !NOMATH_ && !SDWA_),
                 "WIX: ring-of-three kernel only; 6-bit lookups on aligned shards only");
   // > 0: Verify rows' stored vectors are loaded VPF shards before the end of the input
@@ -849,7 +849,7 @@ void rs_apply_lds(ApplyArgs a) {
 #pragma unroll
     for (int r = 0; r < (kVpf ? RT : 1); ++r) vpre[r] = make_uint4(0, 0, 0, 0);
 
-    if constexpr (P::REALIGN) {
+    if constexpr (P::REALIGN && P::WIX != 3) {
       static_assert(!P::NOMATH, "REALIGN: no NOMATH form");
       auto lda = [&](int i) { return ld_aligned<P>(in[i], v0, a.nvec); };
       if constexpr (P::REALIGN == 5) {
@@ -917,27 +917,38 @@ void rs_apply_lds(ApplyArgs a) {
       // per case (a load skipped on a runtime condition, or a join after one, makes the
       // compiler wait for every load in flight; so do the rotation copies of a ring). Set A
       // is consumed while set B loads and vice versa: 2G loads in flight. K >= G.
+      // (REALIGN 2 with WIX 3: the realigning kernel's aligned loads double-buffered the
+      // same way, each vector realigned when its group is consumed)
       constexpr int G = P::WIX == 3 ? 3 : 2;
       const int KG = K / G, rem = K - G * KG;
       const uint32_t tb = 32u * W;
       uint4 A[G], B[G];
+      auto ldx = [&](int i) {
+        if constexpr (P::REALIGN != 0) return ld_aligned<P>(in[i], v0, a.nvec);
+        else return ld(i);
+      };
       auto load_g = [&](uint4 (&x)[G], int i0) {
 #pragma unroll
-        for (int j = 0; j < G; ++j) x[j] = ld(i0 + j);
+        for (int j = 0; j < G; ++j) x[j] = ldx(i0 + j);
         __builtin_amdgcn_sched_barrier(0);  // the loads stay ahead of the lookups
       };
       auto mac_g = [&](const uint4 (&x)[G], int i0, int n) {
         const uint32_t b = lds0 + static_cast<uint32_t>(i0) * tb;
 #pragma unroll
         for (int j = 0; j < G; ++j)
-          if (j < n) lds_mac<RT>(acc, x[j], b + static_cast<uint32_t>(j) * tb);
+          if (j < n) {
+            if constexpr (P::REALIGN != 0)
+              lds_mac<RT>(acc, realign_sel(in[i0 + j], x[j]), b + static_cast<uint32_t>(j) * tb);
+            else
+              lds_mac<RT>(acc, x[j], b + static_cast<uint32_t>(j) * tb);
+          }
       };
       auto load_rem = [&](uint4 (&x)[G], int i0, int n) {  // n = 1 .. G - 1, uniform
         if (n == 1) {
-          x[0] = ld(i0);
+          x[0] = ldx(i0);
         } else {
-          x[0] = ld(i0);
-          x[1] = ld(i0 + 1);
+          x[0] = ldx(i0);
+          x[1] = ldx(i0 + 1);
         }
         __builtin_amdgcn_sched_barrier(0);
       };

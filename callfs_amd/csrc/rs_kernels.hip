@@ -108,6 +108,11 @@ using LdsRealignTriPolicy =
 template <int R, int ORD>
 using LdsRealign64Policy =
     dev::Policy<6, 1, true, true, false, 512, 2, ORD, 0, false, 5>;
+// ... and the realigning kernel's aligned loads double-buffered in two triple sets
+// (rs_apply.hpp WIX 3 with REALIGN 2), R <= 4 and K >= 6 (kTriDbMinK): A/B instances
+// behind the realign-tri orders
+template <int ORD>
+using LdsRealignTriDbPolicy = dev::Policy<5, 1, true, true, false, 512, 2, ORD, 0, false, 2, false, 0, 0, 3>;
 template <int ORD>
 using LdsRealignOutPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 2>;
 template <int ORD>
@@ -331,6 +336,11 @@ template <int ORD, int... Rs>
 constexpr auto lds_realign_tri_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignTriPolicy<Rs + 1, ORD>>...};
 }
+// [consecutive, X8, X32][R - 1], R <= 4
+const std::array<std::array<VecFn, 4>, 3> kLdsRealignTriDb = {
+    lds_order_table<LdsRealignTriDbPolicy<0>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsRealignTriDbPolicy<10>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsRealignTriDbPolicy<11>>(std::make_integer_sequence<int, 4>{})};
 // [consecutive, X8, X32][R - 1]
 const std::array<std::array<VecFn, 8>, 3> kLdsRealignTri = {
     lds_realign_tri_table<0>(std::make_integer_sequence<int, 8>{}),
@@ -729,8 +739,10 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
                         "REALIGN 5 tiles as the plain kernel's");
           fn = kLdsRealign64[realign_order_index(order)][a.R - 1];
         } else if (can_realign(a) && (order >= kOrderRealign || (order < 0 && takes_realign(a)))) {
-          fn = (rtri || (order < 0 && takes_realign_tri(a)) ? kLdsRealignTri : kLdsRealignOut)
-              [realign_order_index(order)][a.R - 1];
+          const bool rt = rtri || (order < 0 && takes_realign_tri(a));
+          fn = (rt ? kLdsRealignTri : kLdsRealignOut)[realign_order_index(order)][a.R - 1];
+          if (rt && a.R <= 4 && a.K >= kTriDbMinK && tridb_enabled())
+            fn = kLdsRealignTriDb[realign_order_index(order)][a.R - 1];
           gx = dev::vec_grid<LdsRealignOutPolicy<0>>(a.nvec, a.batch);
           a.tail_in_vec = 1;  // its first tile writes every edge byte, the tail included
           tail0 = a.S;
