@@ -203,6 +203,10 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     if (tps <= 1024) return q8;
     return pow2_16_32 ? q16 : -1;
   }
+  // R 5..8 on shards up to 256 KiB: the rotating triples in X32 for any K (round 4,
+  // planar 1 MiB objects, tools/small_r8_probe.sh, profiles/r04/smallr8/ab.jsonl: RS(32,8)
+  // 32 KiB 65.9 -> 69.3, one-block layout 66.9 -> 68.7; RS(16,8) 64 KiB 69.8 -> 73.2)
+  if (tps <= 32 && R >= 5 && !read_only) return x32;
   if (K > 12) return -1;
   if (tps <= 32) return K <= 6 || R >= 5 ? x32 : -1;
   if (read_only) return x32;

@@ -310,6 +310,8 @@ int main() {
     CHECK(tri_rule(12, 4, false, false, false, t1));
     CHECK(tri_rule(16, 4, false, false, false, t1));  // double-buffered from K = 6 at R <= 4
     CHECK(!tri_rule(16, 8, false, false, false, t1)); // rotating form: K <= 12
+    CHECK(tri_rule(32, 8, false, false, false, tps_of(32768)));   // ... any K up to 256 KiB
+    CHECK(tri_rule(16, 8, false, false, false, tps_of(65536)));
     CHECK(!tri_rule(4, 2, true, false, false, t1));   // Split layout: realigning kernel
     CHECK(tri_rule(6, 3, false, true, false, t1));    // written + Verify rows: early compares
     CHECK(!tri_rule(6, 6, false, true, false, t1));   // ... at R <= 4 only

@@ -1355,6 +1355,8 @@ def test_plan_wix_triples_vs_oracle(native_lib, k, m, S, order):
     (4, 2, (4 << 20) + 7, (1,)),         # K <= 4, written + Verify rows: X32, early compares
     (10, 4, 1 << 20, (5,)),              # one-erasure decode of the bench shape: G2
     (6, 3, (16 << 20) + 48, ()),         # read-only above 2 MiB: X32
+    (32, 8, 32_768, None),               # R 5..8 up to 256 KiB: rotating triples at any K
+    (16, 8, 65_536 + 9, None),           # ... with a ragged tail
 ])
 def test_plan_rule_triples_vs_oracle(native_lib, k, m, S, erase):
     """The rule's triple-load kernel (tile_order.hpp tri_rule_order: 4 <= K <= 12, R <= 8;
