@@ -198,6 +198,12 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     if (tps <= 32) return x32;
     if (K == 6) return tps <= 1024 ? x32 : x8;
     if (tps <= 128) return K > 16 && addr_tz < 16 ? -1 : g2;
+    // K >= 10 on 1-8 MiB shards at pitches that are not a power of two: the ring of three in
+    // consecutive order (round 4, fourth session, tools/mid_shard_probe.sh,
+    // profiles/r04/mid1/, two passes, one-block layout, tri-Q8 -> ring: RS(10,4) 1.68 MB
+    // 74.2 -> 75.2, 6.7 MB 73.2 -> 74.0, RS(12,4) 1.4 MB 73.2 -> 75.2, 5.6 MB 71.4 -> 74.9;
+    // power-of-two pitches keep tri-Q8: RS(8,4) 2 MiB 77.2 vs 75.0, 4 MiB 74.9 vs 72.2)
+    if (K >= 10 && addr_tz < 20) return -1;
     if (tps <= 256) return q8;
     if (K > 12) return -1;  // 2 MiB and up with K > 12: the ring (RS(16,4) 4 MiB)
     if (tps <= 1024) return q8;

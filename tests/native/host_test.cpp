@@ -321,8 +321,9 @@ int main() {
     CHECK(tri_rule(4, 2, false, false, false, tps_of(256 << 10)));    // small S, few inputs
     CHECK(tri_rule(10, 4, false, false, false, tps_of(104858)));      // small S, double-buffered
     CHECK(tri_rule(10, 8, false, false, false, tps_of(104858)));      // small S, R = 8
-    CHECK(tri_rule(10, 4, false, false, false, tps_of(4 * MiB)));     // double-buffered, Q8
-    CHECK(tri_rule(10, 4, false, false, false, tps_of(6710887)));     // configs[2] shards
+    CHECK(tri_rule(10, 4, false, false, false, tps_of(4 * MiB), 22));  // double-buffered, Q8
+    CHECK(!tri_rule(10, 4, false, false, false, tps_of(6710887), 8));  // configs[2] shards: ring
+    CHECK(tri_rule(8, 4, false, false, false, tps_of(6710887), 8));    // K < 10 keeps Q8
     CHECK(!tri_rule(16, 4, false, false, false, tps_of(4 * MiB)));    // K > 12 above 2 MiB
     // round 4: K <= 5 in X32 up to 8 MiB (RS(4,2) 8 MiB 70.0 -> 79.6), X8 above (16 MiB
     // 71.7 -> 81.1, 32 MiB 77.5 -> 81.4)
@@ -332,7 +333,8 @@ int main() {
     // K 5..6: X32 up to 2 MiB, Q16 above (RS(6,3) 4 MiB 71.7 -> 77.3, 16 MiB 73.2 -> 76.5)
     CHECK(tro(6, 3, MiB, 20) == X32 && tro(6, 3, 2796203, 8) == X32 && tro(6, 3, 16 * MiB, 24) == X8);
     CHECK(tro(6, 6, 2796203, 8) == Q16);  // R 5..8: the rotating form's K = 6 rule
-    CHECK(tro(10, 4, 104858, 8) == X32 && tro(10, 4, 1677722, 8) == static_cast<int>(TileOrder::kSeg8));
+    CHECK(tro(10, 4, 104858, 8) == X32 && tro(10, 4, 1677722, 8) == -1 &&
+          tro(10, 4, 2 * MiB, 21) == static_cast<int>(TileOrder::kSeg8));
     // K 7..12: Q16 on 16-32 MiB power-of-two pitches, round 3's rule elsewhere
     CHECK(tro(10, 4, 16 * MiB, 24) == Q16 && tro(12, 4, 32 * MiB, 25) == Q16);
     CHECK(tro(10, 4, 16 * MiB, 8) == -1 && tro(10, 4, 64 * MiB, 26) == -1);
