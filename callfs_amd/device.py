@@ -1,9 +1,10 @@
 """Device-resident stripes: plans over shards already in HBM.
 
 A *stripe* is one object's n = k+m shards. `StripeBatch` lays a batch of stripes out
-in one device allocation, `[batch][n][pitch]` bytes (pitch = S rounded up to 256 B so
-every shard starts 16-B aligned for the vector kernel), which is the layout the
-benchmark and the GPU tests use. `Plan` wraps rs_plan_create/rs_plan_launch: the
+in HBM: by default in one allocation, `[batch][n][pitch]` bytes (pitch = S rounded up to
+256 B so every shard starts 16-B aligned for the vector kernel), the layout the GPU
+tests use; the benchmark's `planar` layout keeps the data shards and the parity in two
+regions, and the Split layouts reproduce upstream's (see the class). `Plan` wraps rs_plan_create/rs_plan_launch: the
 coefficient tables and shard-pointer tables are uploaded once, and each launch only
 enqueues kernels on the given stream (capturable in a HIP graph).
 
