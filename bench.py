@@ -70,10 +70,13 @@ def parse_args(argv=None):
                         "4: 256-B shard pitch, every stripe's data shards in one region and its "
                         "parity in another), 'pitch' (the same pitch, each stripe's n shards in one "
                         "block: rounds 1-3), or an upstream Split layout (--split-layout)")
+    p.add_argument("--pitch", type=int, default=None,
+                   help="shard pitch in bytes for --layout planar / pitch (a multiple of 16, "
+                        ">= S; default: the library's planar_pitch rule, DESIGN.md §4)")
     p.add_argument("--decode-into", default="fresh", choices=("fresh", "inplace"),
-                   help="with --layout planar: rebuild the erased shards into a region of "
-                        "their own ('fresh', as reedsolomon's Reconstruct allocates missing "
-                        "shards) or into their slots of the batch ('inplace')")
+                   help="with --layout planar or readall: rebuild the erased shards into a "
+                        "region of their own ('fresh', as reedsolomon's Reconstruct allocates "
+                        "missing shards) or into their slots of the batch ('inplace')")
     p.add_argument("--layout-ab", type=int, default=1,
                    help="1: with --layout planar, also time the same workload's kernels in the "
                         "'pitch' layout in this process (tuned as well): line['layout_ab']")
@@ -134,7 +137,7 @@ def dist_env():
     return rank, world, local
 
 
-def cpu_baseline(sb, k, m, erase, seconds, ws_bytes, threads, all_threads=0):
+def cpu_baseline(sb, k, m, erase, seconds, ws_bytes, threads, all_threads=0, rebuilt=None):
     """Reference CPU path (port) timed natively on >= ws_bytes of the GPU's own stripes.
 
     oracle/rs_oracle.c orc_bench_codec runs upstream's per-object work -- Encode
@@ -148,7 +151,9 @@ def cpu_baseline(sb, k, m, erase, seconds, ws_bytes, threads, all_threads=0):
     process may run on, beside the per-GPU share `value` is quoted at.
     Before timing, every sampled stripe is checked
     bit-exactly: CPU parity of the GPU's data == the GPU's parity, and the CPU
-    reconstruction of the erased shards == the GPU's."""
+    reconstruction of the erased shards == the GPU's. With `rebuilt` (the decode writes
+    into fresh buffers, [stripe][erased][pitch]) the host sample's erased shards are the
+    GPU-rebuilt ones, so the CPU reconstruction is compared with the GPU's own output."""
     import numpy as np
     from oracle import cref
 
@@ -156,6 +161,8 @@ def cpu_baseline(sb, k, m, erase, seconds, ws_bytes, threads, all_threads=0):
     stripe_bytes = n * S
     ns = max(1, min(sb.batch, -(-ws_bytes // stripe_bytes)))
     host = sb.gather(ns).cpu().numpy()  # GPU-encoded + GPU-decoded stripes, [ns][n][S]
+    if rebuilt is not None and erase:
+        host[:, erase, :S] = rebuilt[:ns, :, :S].cpu().numpy()
     present = [i not in erase for i in range(k + m)]
 
     # bit-exact checks on all ns stripes
@@ -202,8 +209,11 @@ def cpu_baseline(sb, k, m, erase, seconds, ws_bytes, threads, all_threads=0):
         "sample": (f"{ns} stripes x RS({k},{m}) x {S} B shards ({ns * stripe_bytes / 2**30:.2f} GiB, "
                    f"rotated), encode + decode(erase {sorted(erase)}), ~{seconds / 2:.0f} s per "
                    "threading"),
-        "parity_check": (f"GPU parity and GPU reconstruction == CPU port, bit-exact, on all "
-                         f"{ns} sampled stripes"),
+        "parity_check": (f"GPU parity == CPU port of the GPU's data shards"
+                         + (" (the GPU-rebuilt ones in the erased slots)" if rebuilt is not None
+                            and erase else "")
+                         + f", and the CPU reconstruction of the erased shards == the GPU's, "
+                         f"bit-exact, on all {ns} sampled stripes"),
     }
     if extra:
         out["modes"].update(extra)
@@ -251,10 +261,17 @@ def plan_ceilings(enc, dec, stream):
     each run at their own best rate, the achievable denominator -- and the production
     kernel's no-lookup form. Timed after the bench's timed steps; the plans are relaunched
     afterwards (decode first, then encode) so every shard holds its true bytes again."""
+    from callfs_amd import _native as N
     out = {}
     for name, plan in (("decode", dec), ("encode", enc)):
         ms = {mode: _launch_ms(lambda evs: plan.launch_ceiling(mode, stream, events=evs), stream)
-              for mode in ("read", "write", "nolookup")}
+              for mode in ("read", "write")}
+        try:  # the no-lookup form: A/B build of the library only (CALLFS_RS_LIB)
+            ms["nolookup"] = _launch_ms(
+                lambda evs: plan.launch_ceiling("nolookup", stream, events=evs), stream)
+        except N.NativeError as e:
+            if e.code != N.RS_E_UNSUPPORTED:
+                raise
         plan.corrupt(stream)  # the no-lookup form's Verify rows compare junk: clear
         plan.launch(stream)
         if plan.corrupt(stream):
@@ -263,13 +280,13 @@ def plan_ceilings(enc, dec, stream):
     return out
 
 
-def layout_ab(k, m, S, B, dev, present, stream, tune):
+def layout_ab(k, m, S, B, dev, present, stream, tune, pitch=None):
     """The same encode and decode in the 'pitch' layout (256-B shard pitch, each stripe's n
     shards in one block, the bench layout of rounds 1-3), timed in this process after the
     bench's own plans: a second batch, its plans tuned as the bench's are, mean kernel time
     of 20 event-timed launches after >= 30 ms of warmup each (_launch_ms)."""
     from callfs_amd.device import Plan, StripeBatch
-    sb = StripeBatch(k, m, S, B, dev, layout="pitch")
+    sb = StripeBatch(k, m, S, B, dev, layout="pitch", pitch=pitch)
     sb.fill_random(0x5EED)
     enc, dec = Plan.for_batch(sb), Plan.for_batch(sb, present=present)
     enc.launch(stream)
@@ -320,8 +337,9 @@ def ceiling_entry(ceil, name, nbytes, achieved):
 
 
 def nolookup_entry(ceil, name, nbytes, achieved):
-    """The production kernel's no-lookup form (same loads, stores, grid, order)."""
-    if not ceil:
+    """The production kernel's no-lookup form (same loads, stores, grid, order); timed with
+    the A/B build of the library only."""
+    if not ceil or "nolookup" not in ceil[name]:
         return None
     gbs = nbytes / (ceil[name]["nolookup"] * 1e-3) / 1e9
     return {"kernel": "rs_apply_lds NOMATH form (lookups replaced by one XOR per dword)",
@@ -364,18 +382,19 @@ def main(argv=None):
     present = [i not in erase for i in range(k + m)]
 
     layout = args.split_layout or args.layout
-    sb = StripeBatch(k, m, S, B, dev, layout=layout)
+    sb = StripeBatch(k, m, S, B, dev, layout=layout,
+                     pitch=args.pitch if layout in ("planar", "pitch") else None)
     sb.fill_random(0xCA11F5 + rank)
     enc = Plan.for_batch(sb)
-    # decode into fresh buffers (layout planar, --decode-into fresh): the erased shards are
-    # rebuilt into their own region, as reedsolomon's Reconstruct allocates the missing
-    # shards of a download (codec.go:55) instead of writing over survivors' neighbours;
-    # otherwise into the erased shards' own slots of the batch
-    fresh = layout == "planar" and args.decode_into == "fresh" and erase
+    # decode into fresh buffers (layout planar or readall, --decode-into fresh): the erased
+    # shards are rebuilt into their own region, as reedsolomon's Reconstruct allocates the
+    # missing shards of a download (codec.go:55) instead of writing over survivors'
+    # neighbours; otherwise into the erased shards' own slots of the batch
+    fresh = layout in ("planar", "readall") and args.decode_into == "fresh" and erase
     rebuilt = None
     if fresh:
         from callfs_amd.device import _aligned_empty
-        rebuilt = _aligned_empty((B, len(erase), sb.pitch), 256, dev)
+        rebuilt = _aligned_empty((B, len(erase), sb.par_pitch), 256, dev)
         ptrs = sb.pointers()
         for b in range(B):
             for j, i in enumerate(erase):
@@ -536,26 +555,28 @@ def main(argv=None):
         },
         "cpu_baseline": None,
     }
-    if layout == "planar" and args.layout_ab:
-        line["layout_ab"] = layout_ab(k, m, S, B, dev, present, stream, args.tune)
-        line["layout_ab"]["planar"] = {"encode_frac": line["roofline"]["frac"],
-                                       "decode_frac": line["roofline_decode"]["frac"]}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         visible = len(os.sched_getaffinity(0))
         threads = args.cpu_threads or max(1, min(CPU_SHARE, visible))
         line["cpu_baseline"] = cpu_baseline(sb, k, m, erase, args.cpu_seconds,
-                                            args.cpu_working_set, threads, all_threads=visible)
+                                            args.cpu_working_set, threads, all_threads=visible,
+                                            rebuilt=rebuilt)
         line["cpu_baseline"]["cores_visible"] = visible
-        if fresh:
-            line["cpu_baseline"]["parity_check"] += (
-                "; the decode rebuilds into fresh buffers, checked == the original shards "
-                "on the device after the timed run, and the CPU reconstruction == the "
-                "same originals")
         if threads < visible:
             line["cpu_baseline"]["threads_note"] = (
                 f"{threads} of {visible} visible cores: the GPU box's CPU share per GPU is "
                 f"{CPU_SHARE} (its affinity mask shows the whole host); --cpu-threads "
                 "overrides")
+    if layout == "planar" and args.layout_ab and world == 1 and not S_obj:
+        # (one process only: a second resident batch beside the first; freed buffers first)
+        del rebuilt
+        torch.cuda.empty_cache()
+        try:
+            line["layout_ab"] = layout_ab(k, m, S, B, dev, present, stream, args.tune, args.pitch)
+            line["layout_ab"]["planar"] = {"encode_frac": line["roofline"]["frac"],
+                                           "decode_frac": line["roofline_decode"]["frac"]}
+        except (RuntimeError, SystemExit) as e:  # recorded, never at the cost of the line
+            line["layout_ab"] = {"error": str(e)[:300]}
     if rank == 0:
         print(json.dumps(line), flush=True)
     enc.close()

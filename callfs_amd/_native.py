@@ -11,7 +11,9 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcallfs_rs.so")
+# CALLFS_RS_LIB names another build of the same ABI (the development tools' A/B build,
+# callfs_amd/build.py --ab); the product is libcallfs_rs.so
+LIB_PATH = os.environ.get("CALLFS_RS_LIB") or os.path.join(HERE, "libcallfs_rs.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

@@ -14,6 +14,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcallfs_rs.so")
+# The A/B build (rs_kernels.hpp CALLFS_RS_AB_INSTANCES): the product plus the measurement-only
+# kernel forms and toggles, for the development tools (CALLFS_RS_LIB=<this path>).
+LIB_AB = os.path.join(HERE, "libcallfs_rs_ab.so")
 # Per-kernel register / scratch / occupancy report of the last build (the compiler's
 # kernel-resource-usage remarks), checked by tests/test_kernel_resources.py: the LDS
 # kernel's speed depends on its waves per SIMD.
@@ -38,24 +41,28 @@ def _digest() -> str:
     return h.hexdigest()
 
 
-def _stale() -> bool:
+def _stale(lib: str = LIB) -> bool:
     """Content-hash check (mtimes are not reliable across repo snapshots)."""
     try:
-        with open(LIB + ".sha256") as fh:
-            return not os.path.exists(LIB) or fh.read().strip() != _digest()
+        with open(lib + ".sha256") as fh:
+            return not os.path.exists(lib) or fh.read().strip() != _digest()
     except OSError:
         return True
 
 
-def build(force: bool = False, extra_flags=None) -> str:
-    if not force and not _stale():
-        return LIB
+def build(force: bool = False, extra_flags=None, ab: bool = False) -> str:
+    """Builds libcallfs_rs.so (ab=False) or the A/B build libcallfs_rs_ab.so (ab=True)."""
+    lib = LIB_AB if ab else LIB
+    if not force and not _stale(lib):
+        return lib
     objs = []
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
              "-Wno-unused-result", "-Wno-cuda-compat"] + list(extra_flags or [])
+    if ab:
+        flags.append("-DCALLFS_RS_AB_INSTANCES=1")
     kernels = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
+        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + (".ab.o" if ab else ".o"))
         cmd = [_hipcc(), *flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if src.endswith(".cpp"):
             cmd.insert(1, "-x")
@@ -70,18 +77,20 @@ def build(force: bool = False, extra_flags=None) -> str:
         if r.returncode != 0:
             raise subprocess.CalledProcessError(r.returncode, cmd)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp],
                    check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    with open(RESOURCES, "w") as fh:
-        json.dump({"digest": _digest(), "arch": ARCH, "kernels": kernels}, fh, indent=1)
-        fh.write("\n")
-    with open(LIB + ".sha256", "w") as fh:
+    if not ab:
+        with open(RESOURCES, "w") as fh:
+            json.dump({"digest": _digest(), "arch": ARCH, "instances": len(kernels),
+                       "library_bytes": os.path.getsize(lib), "kernels": kernels}, fh, indent=1)
+            fh.write("\n")
+    with open(lib + ".sha256", "w") as fh:
         fh.write(_digest())
-    return LIB
+    return lib
 
 
 def _parse_resource_remarks(text: str) -> list:
@@ -124,4 +133,4 @@ def _demangle(symbols: list) -> list:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    print(build(force="--force" in sys.argv, ab="--ab" in sys.argv))

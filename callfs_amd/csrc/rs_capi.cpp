@@ -1647,6 +1647,7 @@ int rs_plan_launch_ceiling_timed(rs_plan* plan, void* stream, int mode, void* st
                                  void* stop_event) {
   DeviceGuard dg;
   if (!plan || mode < 0 || mode > 8) return RS_E_ARG;
+  if (!kAbInstances && mode != 1 && mode != 2) return RS_E_UNSUPPORTED;  // (A/B build only)
   HIPCHK(hipSetDevice(plan->device));
   std::vector<int> orders;
   {
@@ -1887,7 +1888,8 @@ int rs_sha256_plan_create(rs_ctx* ctx, int device, const uint8_t* const* msgs,
   plan->device = device;
   plan->count = count;
   plan->mpw = default_msgs_per_wave(count);
-  if (const char* e = std::getenv("CALLFS_SHA_MSGS_PER_WAVE")) plan->mpw = std::atoi(e);
+  if (const char* e = kAbInstances ? std::getenv("CALLFS_SHA_MSGS_PER_WAVE") : nullptr)
+    plan->mpw = std::atoi(e);
   HIPCHK(hipSetDevice(device));
   const size_t bytes = static_cast<size_t>(count) * (sizeof(void*) + sizeof(uint64_t));
   if (count) {

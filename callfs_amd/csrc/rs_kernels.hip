@@ -87,8 +87,8 @@ using LdsVerifyPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, fal
 // byte position of three shards instead of 6; one instance per tile order.
 template <int ORD>
 using LdsWixPolicy = dev::Policy<8, 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, 1>;
-// A/B probe (orders kOrderTri + TileOrder, rs_plan_set_orders only): the same triple loop
-// with nibble lookups, R <= 8
+// The triple loop with nibble lookups, R <= 8 (the rule's triple form, tile_order.hpp
+// tri_rule_order; orders kOrderTri + TileOrder)
 template <int R, int ORD>
 using LdsTriPolicy = dev::Policy<(R <= 4 ? 8 : 2), 1, true, true, false, 512, 2, ORD, 0, false, 0, false, 0, 0, 2>;
 // The triple loop with the Verify rows' compare loads issued with the triple that reaches
@@ -199,7 +199,7 @@ void dispatch(void (*fn)(Args...), dim3 grid, dim3 block, size_t lds, hipStream_
 }
 constexpr int kLdsMinRows = 5;
 constexpr int kLdsMinK = 4;
-constexpr int kPermMaxRows = 8;  // v_perm kernel instantiations (production: k <= 3, R <= 4)
+constexpr int kPermMaxRows = 4;  // v_perm kernel: k <= 3 and R <= 4 (takes_lds sends the rest to LDS)
 
 using VecFn = void (*)(ApplyArgs);
 using ByteFn = void (*)(ApplyArgs, uint64_t);
@@ -247,7 +247,8 @@ const std::array<std::array<VecFn, 4>, kTileOrders> kLdsVerify = {
     lds_order_table<LdsVerifyPolicy<8>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsVerifyPolicy<10>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsVerifyPolicy<11>>(std::make_integer_sequence<int, 4>{})};
-// [tile order][R - 1] for R <= 4, 6-bit triple lookups
+#if CALLFS_RS_AB_INSTANCES
+// [tile order][R - 1] for R <= 4, 6-bit triple lookups (A/B build)
 const std::array<std::array<VecFn, 4>, kTileOrders> kLdsWix = {
     lds_order_table<LdsWixPolicy<0>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsWixPolicy<2>>(std::make_integer_sequence<int, 4>{}),
@@ -256,6 +257,7 @@ const std::array<std::array<VecFn, 4>, kTileOrders> kLdsWix = {
     lds_order_table<LdsWixPolicy<8>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsWixPolicy<10>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsWixPolicy<11>>(std::make_integer_sequence<int, 4>{})};
+#endif
 template <int ORD, int... Rs>
 constexpr auto lds_tri_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsTriPolicy<Rs + 1, ORD>>...};
@@ -299,10 +301,10 @@ const std::array<std::array<VecFn, 4>, 6> kLdsTriDbVerify = {
     lds_order_table<LdsTriDbVerifyPolicy<6>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsTriDbVerifyPolicy<8>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsTriDbVerifyPolicy<10>>(std::make_integer_sequence<int, 4>{})};
-// CALLFS_RS_TRIDB=0 keeps R <= 4 triple launches on the rotating loop (A/B)
+// CALLFS_RS_TRIDB=0 keeps R <= 4 triple launches on the rotating loop (A/B build only)
 bool tridb_enabled() {
   static const bool on = [] {
-    const char* e = std::getenv("CALLFS_RS_TRIDB");
+    const char* e = kAbInstances ? std::getenv("CALLFS_RS_TRIDB") : nullptr;
     return !(e && *e == '0');
   }();
   return on;
@@ -315,11 +317,13 @@ constexpr int kTriDbMinK = 6;
 // tiles per stripe, gained 0.4-1.3 points); on long stripes that put the grid's last tile
 // behind the tail's load chain (tools/tail_ab.sh, profiles/r04/tail_ab: RS(20,4) S =
 // 3,355,444, 410 tiles, first tile 73.8 %, last tile 72.6). CALLFS_RS_TAIL_LAST_TPS
-// overrides the bound (A/B).
+// overrides the bound (A/B build only; clamped so that (tps - 1) << 2 fits the 32-bit code).
+// Every LDS policy that takes this code tiles as LdsPolicy does (static_assert in
+// launch_apply); the realigning forms place their edges themselves (tail_in_vec = 1).
 uint32_t tail_code(uint64_t nvec, uint64_t TV, uint64_t BS) {
   static const uint64_t max_tps = [] {
-    const char* e = std::getenv("CALLFS_RS_TAIL_LAST_TPS");
-    return e && *e ? std::strtoull(e, nullptr, 10) : 32ull;
+    const char* e = kAbInstances ? std::getenv("CALLFS_RS_TAIL_LAST_TPS") : nullptr;
+    return std::min<uint64_t>(e && *e ? std::strtoull(e, nullptr, 10) : 32ull, 1ull << 29);
   }();
   const uint64_t tps = (nvec + TV - 1) / TV, last = nvec - (tps - 1) * TV;
   if (tps <= max_tps && last + 64 <= BS) return static_cast<uint32_t>(((tps - 1) << 2) | 3u);
@@ -336,25 +340,29 @@ template <int ORD, int... Rs>
 constexpr auto lds_realign_tri_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignTriPolicy<Rs + 1, ORD>>...};
 }
-// [consecutive, X8, X32][R - 1], R <= 4
+#if CALLFS_RS_AB_INSTANCES
+// [consecutive, X8, X32][R - 1], R <= 4 (A/B build)
 const std::array<std::array<VecFn, 4>, 3> kLdsRealignTriDb = {
     lds_order_table<LdsRealignTriDbPolicy<0>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsRealignTriDbPolicy<10>>(std::make_integer_sequence<int, 4>{}),
     lds_order_table<LdsRealignTriDbPolicy<11>>(std::make_integer_sequence<int, 4>{})};
+#endif
 // [consecutive, X8, X32][R - 1]
 const std::array<std::array<VecFn, 8>, 3> kLdsRealignTri = {
     lds_realign_tri_table<0>(std::make_integer_sequence<int, 8>{}),
     lds_realign_tri_table<10>(std::make_integer_sequence<int, 8>{}),
     lds_realign_tri_table<11>(std::make_integer_sequence<int, 8>{})};
+#if CALLFS_RS_AB_INSTANCES
 template <int ORD, int... Rs>
 constexpr auto lds_realign64_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealign64Policy<Rs + 1, ORD>>...};
 }
-// [consecutive, X8, X32][R - 1]
+// [consecutive, X8, X32][R - 1] (A/B build)
 const std::array<std::array<VecFn, 8>, 3> kLdsRealign64 = {
     lds_realign64_table<0>(std::make_integer_sequence<int, 8>{}),
     lds_realign64_table<10>(std::make_integer_sequence<int, 8>{}),
     lds_realign64_table<11>(std::make_integer_sequence<int, 8>{})};
+#endif
 template <int ORD, int... Rs>
 constexpr auto lds_realign_out_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignOutPolicyFor<Rs + 1, ORD>>...};
@@ -432,7 +440,7 @@ TileOrder vec_rule(const ApplyArgs& a) {
 // loads and stores; A/B)
 bool realign_out_enabled() {
   static const bool on = [] {
-    const char* e = std::getenv("CALLFS_RS_REALIGN");
+    const char* e = kAbInstances ? std::getenv("CALLFS_RS_REALIGN") : nullptr;
     return !(e && *e == '0');
   }();
   return on;
@@ -452,10 +460,10 @@ bool can_realign(const ApplyArgs& a) {
 bool can_wix(const ApplyArgs& a) {
   return a.R <= 4 && a.K >= 3 && a.K <= 96 && !(a.in_misalign | a.out_misalign);
 }
-// CALLFS_RS_WIX=0 keeps every launch on the ring-of-three nibble kernel (A/B)
+// CALLFS_RS_WIX=0 keeps every launch on the ring-of-three nibble kernel (A/B build only)
 bool wix_enabled() {
   static const bool on = [] {
-    const char* e = std::getenv("CALLFS_RS_WIX");
+    const char* e = kAbInstances ? std::getenv("CALLFS_RS_WIX") : nullptr;
     return !(e && *e == '0');
   }();
   return on;
@@ -488,9 +496,12 @@ bool wix_enabled() {
 // RS(12,4) 5,592,406 B 71.8 -> 74.2 (X8), RS(4,2) 1,048,577 B 71.0 -> 71.9. With unaligned
 // stores as well (the contiguous Split layout) the same forms lost 1-6 points
 // (split_enc.jsonl), so misaligned outputs keep the realigning kernel.
+// (Measured for K <= 12 only; wider launches above 256 KiB shards keep the realigning
+// kernel, as the aligned rule keeps K > 12 off the triples there.)
 int tri_unaligned_order(const ApplyArgs& a, uint64_t tps) {
   if (a.R > 8 || a.K < 4 || !a.in_misalign || a.out_misalign || tile_order_override() >= 0)
     return -1;
+  if (a.K > 12 && tps > 32) return -1;
   return static_cast<int>(tps <= 256 ? TileOrder::kXcd32 : TileOrder::kXcd8);
 }
 
@@ -530,7 +541,7 @@ bool takes_realign(const ApplyArgs& a) {
 }
 // the 64-vector realigning form: misaligned inputs, every output 16-B aligned
 bool can_realign64(const ApplyArgs& a) {
-  return can_realign(a) && a.in_misalign && !a.out_misalign;
+  return kAbInstances && can_realign(a) && a.in_misalign && !a.out_misalign;
 }
 
 // The rule's realigning launches with triple loads (tile_order.hpp realign_tri_rule);
@@ -598,10 +609,10 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       add(realign_in(TileOrder::kXcd32));
       add(realign_in(TileOrder::kConsecutive));
       if (every_instance) add(realign_in(TileOrder::kXcd8));
-      if (can_realign64(a)) {
+      if (every_instance && can_realign64(a)) {  // (A/B build)
         add(r64_in(TileOrder::kXcd32));
         add(r64_in(TileOrder::kConsecutive));
-        if (every_instance) add(r64_in(TileOrder::kXcd8));
+        add(r64_in(TileOrder::kXcd8));
       }
       if (a.K >= 3) {  // the realigning kernel with triple loads
         add(rtri_in(TileOrder::kXcd32));
@@ -637,7 +648,7 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       if (tps > 1024 || (every_instance && tps >= 64)) add(tri_in(TileOrder::kSeg16));
       if (tps > 1024 || every_instance) add(tri_in(TileOrder::kXcd8));
     }
-    if (every_instance && can_wix(a)) {  // WIX: A/B instances only
+    if (kAbInstances && every_instance && can_wix(a)) {  // WIX: A/B build only
       const int n0 = static_cast<int>(c.size());
       for (int i = 0; i < n0; ++i)
         if (c[i] >= 0 && c[i] < kTileOrders) add(wix_in(static_cast<TileOrder>(c[i])));
@@ -663,7 +674,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   if (order >= kOrderRealignTri) order = rtri ? order - kOrderRealignTri + kOrderRealign : -1;
   bool tri = order >= kOrderTri && a.R <= 8 && a.K >= 3;
   if (order >= kOrderTri) order = tri ? order - kOrderTri : -1;
-  const bool wix = order >= kOrderWix && can_wix(a);
+  const bool wix = kAbInstances && order >= kOrderWix && can_wix(a);
   if (order >= kOrderWix) order -= kOrderWix;
   uint64_t tail0 = 0;
   a.tail_in_vec = 0;
@@ -695,10 +706,14 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
           const int oi = static_cast<int>(ord);
           if (a.R <= 4 && (a.verify_mask & rows) && oi >= 0 && oi < kTileOrders)
             fn = kLdsVerify[oi][a.R - 1];
+#if CALLFS_RS_AB_INSTANCES
           if (wix && oi >= 0 && oi < kTileOrders) {  // (at most 56 KiB of tables at K = 96)
             fn = kLdsWix[oi][a.R - 1];
             lds = dev::lds_bytes_wix(a.K);
           }
+#else
+          (void)wix;
+#endif
           if (!tri && order < 0 && takes_tri(a)) tri = true;  // the rule: ord is the nibble rule's
           if (tri) {
             const int ti = tri_index(order < 0 ? static_cast<TileOrder>(tri_rule_of(a)) : ord);
@@ -729,20 +744,37 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
                           LdsVerifyPolicy<0>::TILE_VECS == LdsPolicy::TILE_VECS &&
                           LdsRealignOutPolicy<0>::BS == LdsPolicy::BS &&
                           LdsRealignOut8Policy<0>::TILE_VECS == LdsRealignOutPolicy<0>::TILE_VECS &&
-                          LdsRealignOutPolicy<10>::TILE_VECS == LdsRealignOutPolicy<0>::TILE_VECS,
-                      "one grid shape for every LDS policy");
+                          LdsRealignOutPolicy<10>::TILE_VECS == LdsRealignOutPolicy<0>::TILE_VECS &&
+                          LdsTriPolicy<1, 0>::TILE_VECS == LdsPolicy::TILE_VECS &&
+                          LdsTriPolicy<8, 10>::TILE_VECS == LdsPolicy::TILE_VECS &&
+                          LdsTriPolicy<8, 10>::BS == LdsPolicy::BS &&
+                          LdsTriDbPolicy<0>::TILE_VECS == LdsPolicy::TILE_VECS &&
+                          LdsTriDbPolicy<0>::BS == LdsPolicy::BS &&
+                          LdsTriVerifyPolicy<0>::TILE_VECS == LdsPolicy::TILE_VECS &&
+                          LdsTriVerifyPolicy<0>::BS == LdsPolicy::BS &&
+                          LdsTriDbVerifyPolicy<0>::TILE_VECS == LdsPolicy::TILE_VECS &&
+                          LdsTriDbVerifyPolicy<0>::BS == LdsPolicy::BS &&
+                          LdsVerifyPolicy<0>::BS == LdsPolicy::BS &&
+                          LdsWixPolicy<0>::TILE_VECS == LdsPolicy::TILE_VECS &&
+                          LdsWidePolicy::TILE_VECS == LdsPolicy::TILE_VECS &&
+                          LdsWideQ8Policy::TILE_VECS == LdsPolicy::TILE_VECS,
+                      "one grid shape and tail placement (tail_code) for every LDS policy");
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         // misaligned shards: the realigning form, unless a tuned order names a plain kernel
         if (r64) {  // 512-vector tiles and the ragged tail as the plain kernel's
           static_assert(LdsRealign64Policy<1, 0>::TILE_VECS == LdsPolicy::TILE_VECS &&
                             LdsRealign64Policy<8, 0>::TILE_VECS == LdsPolicy::TILE_VECS,
                         "REALIGN 5 tiles as the plain kernel's");
+#if CALLFS_RS_AB_INSTANCES
           fn = kLdsRealign64[realign_order_index(order)][a.R - 1];
+#endif
         } else if (can_realign(a) && (order >= kOrderRealign || (order < 0 && takes_realign(a)))) {
           const bool rt = rtri || (order < 0 && takes_realign_tri(a));
           fn = (rt ? kLdsRealignTri : kLdsRealignOut)[realign_order_index(order)][a.R - 1];
+#if CALLFS_RS_AB_INSTANCES
           if (rt && a.R <= 4 && a.K >= kTriDbMinK && tridb_enabled())
             fn = kLdsRealignTriDb[realign_order_index(order)][a.R - 1];
+#endif
           gx = dev::vec_grid<LdsRealignOutPolicy<0>>(a.nvec, a.batch);
           a.tail_in_vec = 1;  // its first tile writes every edge byte, the tail included
           tail0 = a.S;
@@ -793,6 +825,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
 // lookups replaced by one XOR per input dword (DESIGN.md §5 "Traffic ceiling per shape").
 // bench.py times it in the same process as the plan it bounds.
 namespace {
+#if CALLFS_RS_AB_INSTANCES
 template <int ORD, int R>
 using NomathPolicy = dev::Policy<2, 1, true, true, false, 512, (R > 8 ? 4 : 2), ORD, (R > 8 ? 1 : 0), true>;
 template <int ORD, int... Rs>
@@ -814,6 +847,7 @@ const auto kNomathWideQ8 = nomath_wide_table<6>(std::make_integer_sequence<int, 
 static_assert(NomathPolicy<0, 4>::TILE_VECS == LdsPolicy::TILE_VECS &&
                   NomathPolicy<0, 16>::TILE_VECS == LdsPolicy::TILE_VECS && LdsPolicy::BS == 512,
               "the ceilings run the production grid");
+#endif
 
 const std::array<VecFn, kTileOrders> kStreamRead = {
     &dev::rs_stream_read<0>, &dev::rs_stream_read<2>, &dev::rs_stream_read<5>, &dev::rs_stream_read<6>,
@@ -823,6 +857,7 @@ const std::array<VecFn, kTileOrders> kStreamWrite = {
     &dev::rs_stream_write<6>, &dev::rs_stream_write<8>, &dev::rs_stream_write<10>,
     &dev::rs_stream_write<11>};
 
+#if CALLFS_RS_AB_INSTANCES
 // modes 3..5 (probe): the write streams alone from each row's first 64 / 128 / 256-B
 // boundary, consecutive tiles
 const std::array<VecFn, 3> kStreamWriteAligned = {
@@ -830,12 +865,14 @@ const std::array<VecFn, 3> kStreamWriteAligned = {
 // modes 6..8 (probe): the read streams alone from each shard's first 64 / 128 / 256-B boundary
 const std::array<VecFn, 3> kStreamReadAligned = {
     &dev::rs_stream_read<0, 64>, &dev::rs_stream_read<0, 128>, &dev::rs_stream_read<0, 256>};
+#endif
 }  // namespace
 
 hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, LaunchEvents ev) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1 || !a.ltabs ||
       mode < 0 || mode > 8)
     return hipErrorInvalidValue;
+  if (!kAbInstances && mode != 1 && mode != 2) return hipErrorNotSupported;
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
   a.tail_in_vec = a.nvec * 16 < a.S ? tail_code(a.nvec, LdsPolicy::TILE_VECS, LdsPolicy::BS) : 0u;
@@ -857,15 +894,20 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
                  : (order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a));
   const unsigned grid = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
   if (mode > 0) {  // the read streams alone / the write streams alone
+#if CALLFS_RS_AB_INSTANCES
     const VecFn fn = mode >= 6   ? kStreamReadAligned[mode - 6]
                      : mode >= 3 ? kStreamWriteAligned[mode - 3]
                                : (mode == 1 ? kStreamRead : kStreamWrite)[static_cast<int>(ord)];
+#else
+    const VecFn fn = (mode == 1 ? kStreamRead : kStreamWrite)[static_cast<int>(ord)];
+#endif
     a.tail_in_vec = 0;
     launch_sliced(grid, a.K + a.R, a, [&](uint32_t blocks, bool first, bool last) {
       dispatch(fn, dim3(blocks), dim3(LdsPolicy::BS), 0, stream, ev, first, last, a);
     });
     return hipGetLastError();
   }
+#if CALLFS_RS_AB_INSTANCES
   VecFn fn;
   if (a.R <= 8)
     fn = kNomath[static_cast<int>(ord)][a.R - 1];
@@ -879,6 +921,9 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
     dispatch(fn, dim3(blocks), dim3(LdsPolicy::BS), lds, stream, ev, first, last, a);
   });
   return hipGetLastError();
+#else
+  return hipErrorNotSupported;
+#endif
 }
 
 }  // namespace callfs

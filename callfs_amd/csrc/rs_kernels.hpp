@@ -6,7 +6,18 @@
 #include <vector>
 #include <cstdint>
 
+// 1: also build the measurement-only kernel forms (the 6-bit triple lookups, the 64-vector
+// and double-buffered realigning forms, the no-lookup and aligned-window ceilings) and honour
+// the A/B environment toggles (CALLFS_RS_WIX, _TRIDB, _REALIGN, _TAIL_LAST_TPS). The
+// product library is built with 0: `python callfs_amd/build.py --ab` writes the A/B build to
+// libcallfs_rs_ab.so, which the development tools load through CALLFS_RS_LIB.
+#ifndef CALLFS_RS_AB_INSTANCES
+#define CALLFS_RS_AB_INSTANCES 0
+#endif
+
 namespace callfs {
+
+constexpr bool kAbInstances = CALLFS_RS_AB_INSTANCES != 0;
 
 constexpr int kMaxRowsPerLaunch = 16;  // output rows per launch group (LDS kernel above 4)
 constexpr int kMaxK = 256;
@@ -146,7 +157,10 @@ std::vector<int> order_candidates(const ApplyArgs& a, bool every_instance = fals
 //           one XOR per input dword instead of the lookups (outputs junk, Verify rows may
 //           flag status);
 //   mode 1  the launch's read streams alone (inputs + Verify rows; writes nothing);
-//   mode 2  its write streams alone (junk into the written rows).
+//   mode 2  its write streams alone (junk into the written rows);
+//   modes 3..8 (probes) the write / read streams from each row's first 64 / 128 / 256-B
+//           boundary.
+// Modes 0 and 3..8 exist in the A/B build only (hipErrorNotSupported otherwise).
 hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode,
                           LaunchEvents ev = {});
 

@@ -127,7 +127,14 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
   // -> 67.7, RS(12,4) 64 KiB equal)
   if (stripe_stride == (1ull << 20) && tps <= 32) return TileOrder::kGroup2;
   if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
-  if (tps <= 128 || (tps <= 1024 && streams >= 14 && rows >= 5 && !verify)) return TileOrder::kGroup2;
+  // round 5, planar layout (tools/rule_sweep.sh, profiles/r05/rule/): more than 16 inputs
+  // with R <= 4 on 256 KiB - 1 MiB shards run the ring faster in consecutive order
+  // (RS(20,4) 838,861 B G2 73.9 / 73.4 -> consecutive 74.9 / 74.7)
+  if (tps <= 128 && streams - rows > 16 && rows <= 4 && !verify) return TileOrder::kConsecutive;
+  // (round 5, planar: not for more than 16 inputs, RS(32,8) 2 MiB G2 69.3 / 69.2 ->
+  // consecutive 70.4 / 70.7)
+  if (tps <= 128 || (tps <= 1024 && streams >= 14 && rows >= 5 && !verify && streams - rows <= 16))
+    return TileOrder::kGroup2;
   if (tps <= 1024) return TileOrder::kConsecutive;  // S <= 8 MiB, few streams
   if (addr_tz >= 23 && S < (128ull << 20)) {
     if (streams >= 12)
@@ -195,7 +202,8 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     return tps <= 128 ? static_cast<int>(tri_order(nibble)) : -1;
   }
   if (db && !read_only) {  // round 4, double-buffered (profiles/r04/tri_sweep3, tridb_wide)
-    if (tps <= 32) return x32;
+    // (round 5, planar: G2 for K > 16, RS(20,4) 52 KB X32 69.8 / 70.0 -> G2 72.5)
+    if (tps <= 32) return K > 16 ? g2 : x32;
     if (K == 6) return tps <= 1024 ? x32 : x8;
     if (tps <= 128) return K > 16 && addr_tz < 16 ? -1 : g2;
     // K >= 10 on 1-8 MiB shards at pitches that are not a power of two: the ring of three in
@@ -203,16 +211,22 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     // profiles/r04/mid1/, two passes, one-block layout, tri-Q8 -> ring: RS(10,4) 1.68 MB
     // 74.2 -> 75.2, 6.7 MB 73.2 -> 74.0, RS(12,4) 1.4 MB 73.2 -> 75.2, 5.6 MB 71.4 -> 74.9;
     // power-of-two pitches keep tri-Q8: RS(8,4) 2 MiB 77.2 vs 75.0, 4 MiB 74.9 vs 72.2)
-    if (K >= 10 && addr_tz < 20) return -1;
-    if (tps <= 256) return q8;
-    if (K > 12) return -1;  // 2 MiB and up with K > 12: the ring (RS(16,4) 4 MiB)
-    if (tps <= 1024) return q8;
+    // round 5, planar (tools/rule_sweep.sh, tools/cfg12_orders.sh, profiles/r05/): above 1 MiB
+    // the ring in consecutive order for K >= 10 at every pitch (RS(10,4) 2 MiB tri-Q8 72.9 ->
+    // ring 76.9, 4 MiB 74.8 -> 75.4, 8 MiB 72.6 -> 75.6; round 4 kept tri-Q8 on power-of-two
+    // pitches in the one-block layout), except Q16 on 16-32 MiB power-of-two pitches (round 4,
+    // RS(10,4) 16 MiB 73.8 -> 78.7); K 7..9 in G2 to 2 MiB (RS(8,4) 2 MiB Q8 75.1 / 74.1 -> G2
+    // 77.6 / 76.9) and the ring to 8 MiB (RS(8,4) 8 MiB Q8 73.6 / 72.6 -> ring 74.2 / 75.4)
+    if (K >= 10) return K <= 12 && pow2_16_32 ? q16 : -1;
+    if (tps <= 256) return g2;
+    if (tps <= 1024) return -1;
     return pow2_16_32 ? q16 : -1;
   }
   // R 5..8 on shards up to 256 KiB: the rotating triples in X32 for any K (round 4,
   // planar 1 MiB objects, tools/small_r8_probe.sh, profiles/r04/smallr8/ab.jsonl: RS(32,8)
   // 32 KiB 65.9 -> 69.3, one-block layout 66.9 -> 68.7; RS(16,8) 64 KiB 69.8 -> 73.2)
-  if (tps <= 32 && R >= 5 && !read_only) return x32;
+  // (round 5, planar: G2 for K <= 12, RS(8,8) 128 KiB X32 75.4 / 75.5 -> G2 76.3 / 76.5)
+  if (tps <= 32 && R >= 5 && !read_only) return K <= 12 ? g2 : x32;
   if (K > 12) return -1;
   if (tps <= 32) return K <= 6 || R >= 5 ? x32 : -1;
   if (read_only) return x32;
@@ -222,6 +236,12 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
   if (K <= 5) return tps > 1024 ? x8 : x32;
   if (K == 6) return tps <= 256 ? x32 : q16;
   if (pow2_16_32) return q16;
+  // R 5..8 above 1 MiB (round 5, planar, profiles/r05/rule/): to 2 MiB consecutive for K < 10
+  // and Q8 from K = 10 (RS(8,8) 2 MiB tri-G2 73.0 / 73.3 -> tri 74.8 / 74.3, RS(10,8) 1.68 MB
+  // 74.3 -> tri-Q8 74.9), to 8 MiB X32 (RS(10,8) 6.7 MB ring G2 70.2 / 70.2 -> tri-X32 72.3,
+  // RS(8,8) 8 MiB ring 72.6 = tri-X32 72.6 / 72.8)
+  if (R >= 5 && tps > 128)
+    return tps <= 256 ? (K < 10 ? static_cast<int>(TileOrder::kConsecutive) : q8) : tps <= 1024 ? x32 : -1;
   if (tps <= 256) return static_cast<int>(tri_order(nibble));
   return -1;
 }

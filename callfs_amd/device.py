@@ -60,9 +60,13 @@ class StripeBatch:
     BODY_ALIGN = 8192
 
     def __init__(self, k: int, m: int, S: int, batch: int, device: torch.device,
-                 layout: str = "pitch"):
+                 layout: str = "pitch", pitch: Optional[int] = None):
+        """pitch: shard pitch in bytes for the 'pitch', 'planar' and 'shardmajor' layouts
+        (a multiple of 16, at least S; default pitch_for(S), the library's own rule)."""
         if layout not in ("pitch", "split", "readall", "planar", "shardmajor"):
             raise ValueError(f"layout {layout!r}")
+        if pitch is not None and (layout in ("split", "readall") or pitch < S or pitch % 16):
+            raise ValueError(f"pitch {pitch} for layout {layout!r}, S = {S}")
         self.k, self.m, self.S, self.batch = k, m, S, batch
         self.n = k + m
         self.layout = layout
@@ -75,13 +79,13 @@ class StripeBatch:
                 self.body_pitch = -(-k * S // self.BODY_ALIGN) * self.BODY_ALIGN
                 self.par_pitch = -(-S // 64) * 64
             else:
-                self.pitch = self.par_pitch = pitch_for(S)
+                self.pitch = self.par_pitch = pitch or pitch_for(S)
                 self.body_pitch = k * self.pitch
             self.body = _aligned_empty((batch, self.body_pitch), self.BODY_ALIGN, self.device)
             self.par = _aligned_empty((batch, m, self.par_pitch), 256, self.device)
             self.buf = None
             return
-        self.pitch = S if layout == "split" else pitch_for(S)
+        self.pitch = S if layout == "split" else (pitch or pitch_for(S))
         if layout == "shardmajor":
             sm = torch.empty((self.n, batch, self.pitch), dtype=torch.uint8, device=self.device)
             self.buf = sm.permute(1, 0, 2)  # [batch][n][pitch] view of [n][batch][pitch]

@@ -208,7 +208,9 @@ int  rs_plan_set_orders(rs_plan* plan, const int* orders, int n);
  *   RS_CEIL_READ      the plan's read streams alone (k inputs + compared rows);
  *   RS_CEIL_WRITE     its write streams alone.
  * NOLOOKUP and WRITE leave junk in the written shards and NOLOOKUP may flag status:
- * relaunch the plan (and read rs_plan_status) before relying on either. */
+ * relaunch the plan (and read rs_plan_status) before relying on either.
+ * The product library implements READ and WRITE; NOLOOKUP and the probes below exist in
+ * the A/B build of the tools (libcallfs_rs_ab.so) and return RS_E_UNSUPPORTED here. */
 #define RS_CEIL_NOLOOKUP 0
 #define RS_CEIL_READ 1
 #define RS_CEIL_WRITE 2

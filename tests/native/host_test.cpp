@@ -316,14 +316,14 @@ int main() {
     CHECK(tri_rule(6, 3, false, true, false, t1));    // written + Verify rows: early compares
     CHECK(!tri_rule(6, 6, false, true, false, t1));   // ... at R <= 4 only
     CHECK(!tri_rule(10, 9, false, false, false, t1)); // 16-byte entries
-    CHECK(!tri_rule(8, 8, false, false, false, tps_of(8 * MiB)));     // 8 MiB shards: lost
+    CHECK(tri_rule(8, 8, false, false, false, tps_of(8 * MiB), 23));  // 8 MiB, R = 8: X32 (round 5)
     CHECK(tri_rule(8, 4, false, false, false, tps_of(2 * MiB)));      // 2 MiB: gained
     CHECK(tri_rule(4, 2, false, false, false, tps_of(256 << 10)));    // small S, few inputs
     CHECK(tri_rule(10, 4, false, false, false, tps_of(104858)));      // small S, double-buffered
     CHECK(tri_rule(10, 8, false, false, false, tps_of(104858)));      // small S, R = 8
-    CHECK(tri_rule(10, 4, false, false, false, tps_of(4 * MiB), 22));  // double-buffered, Q8
+    CHECK(!tri_rule(10, 4, false, false, false, tps_of(4 * MiB), 22)); // K >= 10 above 1 MiB: ring
     CHECK(!tri_rule(10, 4, false, false, false, tps_of(6710887), 8));  // configs[2] shards: ring
-    CHECK(tri_rule(8, 4, false, false, false, tps_of(6710887), 8));    // K < 10 keeps Q8
+    CHECK(!tri_rule(8, 4, false, false, false, tps_of(6710887), 8));   // K 7..9 above 2 MiB: ring
     CHECK(!tri_rule(16, 4, false, false, false, tps_of(4 * MiB)));    // K > 12 above 2 MiB
     // round 4: K <= 5 in X32 up to 8 MiB (RS(4,2) 8 MiB 70.0 -> 79.6), X8 above (16 MiB
     // 71.7 -> 81.1, 32 MiB 77.5 -> 81.4)
@@ -333,15 +333,24 @@ int main() {
     // K 5..6: X32 up to 2 MiB, Q16 above (RS(6,3) 4 MiB 71.7 -> 77.3, 16 MiB 73.2 -> 76.5)
     CHECK(tro(6, 3, MiB, 20) == X32 && tro(6, 3, 2796203, 8) == X32 && tro(6, 3, 16 * MiB, 24) == X8);
     CHECK(tro(6, 6, 2796203, 8) == Q16);  // R 5..8: the rotating form's K = 6 rule
-    CHECK(tro(10, 4, 104858, 8) == X32 && tro(10, 4, 1677722, 8) == -1 &&
-          tro(10, 4, 2 * MiB, 21) == static_cast<int>(TileOrder::kSeg8));
+    CHECK(tro(10, 4, 104858, 8) == X32 && tro(10, 4, 1677722, 8) == -1 && tro(10, 4, 2 * MiB, 21) == -1);
+    // round 5, planar layout: K 7..9 in G2 to 2 MiB, the ring to 8 MiB; R 5..8: G2 to
+    // 256 KiB (K <= 12), consecutive / Q8 to 2 MiB, X32 to 8 MiB
+    const int Q8 = static_cast<int>(TileOrder::kSeg8), CONS = static_cast<int>(TileOrder::kConsecutive);
+    CHECK(tro(8, 4, 2 * MiB, 21) == G2 && tro(8, 4, 8 * MiB, 23) == -1);
+    CHECK(tro(8, 8, 131072, 17) == G2 && tro(32, 8, 32768, 15) == X32 && tro(8, 8, 2 * MiB, 21) == CONS);
+    CHECK(tro(10, 8, 1677722, 8) == Q8 && tro(10, 8, 6710887, 8) == X32 && tro(8, 8, 8 * MiB, 23) == X32);
+    CHECK(tro(10, 8, 16 * MiB, 8) == -1);
+    CHECK(lds_tile_order(838861, tps_of(838861), 8, 24, 0, false, false, 4) == TileOrder::kConsecutive);
+    CHECK(lds_tile_order(2 * MiB, tps_of(2 * MiB), 21, 40, 0, false, false, 8) == TileOrder::kConsecutive);
+    CHECK(lds_tile_order(524288, tps_of(524288), 19, 40, 0, false, false, 8) == TileOrder::kGroup2);
     // K 7..12: Q16 on 16-32 MiB power-of-two pitches, round 3's rule elsewhere
     CHECK(tro(10, 4, 16 * MiB, 24) == Q16 && tro(12, 4, 32 * MiB, 25) == Q16);
     CHECK(tro(10, 4, 16 * MiB, 8) == -1 && tro(10, 4, 64 * MiB, 26) == -1);
     CHECK(tro(10, 4, MiB, 20) == G2);  // the nibble rule's order (G2 for the bench shape)
     // K > 16 from 256 KiB to 1 MiB: the ring on unaligned pitches, G2 on 64 KiB-aligned ones
     CHECK(tro(20, 4, 838861, 8) == -1 && tro(20, 4, MiB, 20) == G2 && tro(16, 4, 838861, 8) == G2);
-    CHECK(tro(20, 4, 52429, 8) == X32);
+    CHECK(tro(20, 4, 52429, 8) == G2 && tro(16, 4, 65536, 16) == X32);
     // read-only launches: X32 at every size above 256 KiB (RS(6,3) 16 MiB 85.7 -> 90.0)
     CHECK(tro(4, 2, 16 * MiB, 24, true, true) == X32 && tro(10, 4, MiB, 20, true, true, TileOrder::kXcd32) == X32);
     // written + Verify rows (R <= 4, early compares): K <= 4 in X32, K 5..12 up to 1 MiB

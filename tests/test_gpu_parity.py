@@ -1293,52 +1293,11 @@ def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, era
         assert {"x8", "x32"} <= set(taken), taken
         with pytest.raises(N.NativeError):
             plan.set_orders(["realign"])  # aligned shards: no realigning kernel
-    # 6-bit triple lookups: aligned shards, one launch group of R = m <= 4 rows (written
-    # or compared), K >= 4 (the LDS kernel)
-    wix_ok = off % 16 == 0 and S % 16 == 0 and k >= 4 and m <= 4
-    if wix_ok:
-        assert {"wix", "wix-g2", "wix-x32"} <= set(taken), taken
-    else:
-        assert not any(t.startswith("wix") for t in taken), taken
+    # the 6-bit triple lookups (Policy::WIX 1) are A/B-build forms: the product refuses them
+    assert not any(t.startswith("wix") for t in taken), taken
     with pytest.raises(N.NativeError):
         plan.set_orders(["none"] * (plan_groups := int(N.lib.rs_plan_groups(plan.handle))) + ["none"])
     plan.set_orders(["none"] * plan_groups)
-
-
-@pytest.mark.parametrize("k,m,S,order", [
-    (6, 4, 65_536 * 3 + 5, "wix"),        # two triples, no nibble shards
-    (4, 2, 1_000_003, "wix-g2"),           # one triple + 1
-    (5, 3, 262_147, "wix"),                # one triple + 2
-    (10, 4, 1 << 20, "wix"),               # the bench shape: 3 triples + 1
-    (12, 1, 100_000, "wix-x32"),           # R = 1
-    (16, 4, 262_144 + 48, "wix-x8"),
-    (20, 4, 1 << 18, "wix"),
-    (32, 4, 131_073, "wix-g2"),            # ragged tail through the nibble tables
-    (64, 2, 16_384 + 16, "wix"),
-    (96, 3, 8_192, "wix-x32"),             # 32 triples: the largest K offered (56 KiB LDS)
-])
-def test_plan_wix_triples_vs_oracle(native_lib, k, m, S, order):
-    """The 6-bit lookups over shard triples (Policy::WIX): every triple/remainder split
-    (K % 3 = 0, 1, 2), R = 1..4, ragged tails and several tile orders, every byte of
-    every stripe against the oracle's parity; constant stripes (all 0x00 / all 0xFF)
-    as the SURVEY's sanity inputs."""
-    import torch
-    from callfs_amd.device import Plan
-    n, batch = k + m, 3
-    pitch = (S + 255) // 256 * 256
-    buf = torch.randint(0, 256, (batch, n, pitch), dtype=torch.uint8, device="cuda:0")
-    buf[1, :k].fill_(0xFF)
-    buf[2, :k, : S // 2].zero_()
-    ptrs = [buf[b, i].data_ptr() for b in range(batch) for i in range(n)]
-    plan = Plan(k, m, S, batch, ptrs)
-    plan.set_orders([order])
-    plan.launch()
-    torch.cuda.synchronize()
-    h = buf.cpu().numpy()
-    for b in range(batch):
-        want = cref.encode([h[b, i, :S] for i in range(k)], k, m)
-        for j in range(m):
-            assert np.array_equal(h[b, k + j, :S], want[j]), (b, j)
 
 
 @pytest.mark.parametrize("k,m,S,erase", [
@@ -1452,9 +1411,10 @@ def test_plan_tune_misaligned_split_layout(native_lib, k, m, S, batch, off):
 ])
 def test_plan_ceiling_modes_then_relaunch(native_lib, k, m, S, batch, erase):
     """rs_plan_launch_ceiling (bench.py's live roofline denominators): the read-only mode
-    leaves every byte as it was; the no-lookup and write-only modes may overwrite the
-    written rows, and relaunching the plan restores them bit-exactly; bad arguments are
-    refused."""
+    leaves every byte as it was; the write-only mode may overwrite the written rows, and
+    relaunching the plan restores them bit-exactly; bad arguments are refused, and the
+    A/B build's measurement modes (no-lookup, aligned-window probes) are RS_E_UNSUPPORTED
+    in the product library."""
     import ctypes
     import torch
     from callfs_amd import _native as N
@@ -1469,11 +1429,12 @@ def test_plan_ceiling_modes_then_relaunch(native_lib, k, m, S, batch, erase):
     plan.launch_ceiling("read")
     torch.cuda.synchronize()
     assert torch.equal(sb.buf, before)
-    for mode in ("read64", "read128", "read256"):  # alignment probes: read only
-        plan.launch_ceiling(mode)
-        torch.cuda.synchronize()
-        assert torch.equal(sb.buf, before), mode
-    for mode in ("write", "nolookup", "write64", "write128", "write256"):
+    for mode in ("nolookup", "write64", "write128", "write256", "read64", "read128", "read256"):
+        assert N.lib.rs_plan_launch_ceiling(plan.handle, None, Plan.CEILINGS[mode]) == \
+            N.RS_E_UNSUPPORTED, mode
+    torch.cuda.synchronize()
+    assert torch.equal(sb.buf, before)
+    for mode in ("write",):
         plan.launch_ceiling(mode)
         plan.corrupt()  # the no-lookup form compares junk: clear
         plan.launch()
@@ -1535,9 +1496,9 @@ def test_plan_launch_timed_events(native_lib, k, m, S, batch, erase):
 @pytest.mark.parametrize("k,m,S,batch", [(10, 4, 100_003, 3), (4, 2, 65_537, 5)])
 def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m, S, batch):
     """On an upstream Split-layout batch (misaligned shards, pitch = S) the ceiling modes
-    change nothing but the written shards: the write-only modes store aligned blocks from
-    each row's first 16 / 64 / 128 / 256-B boundary on, never a byte of a neighbouring
-    input shard; the plan then restores its outputs bit-exactly."""
+    change nothing but the written shards: the write-only mode stores aligned blocks from
+    each row's first 16-B boundary on, never a byte of a neighbouring input shard; the plan
+    then restores its outputs bit-exactly."""
     import torch
     from callfs_amd.device import Plan, StripeBatch
     sb = StripeBatch(k, m, S, batch, torch.device("cuda:0"), layout="split")
@@ -1545,7 +1506,7 @@ def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m,
     enc = Plan.for_batch(sb)
     enc.launch()
     before = sb.buf.clone()
-    for mode in ("read", "write", "nolookup", "read128", "write64", "write128", "write256"):
+    for mode in ("read", "write"):
         enc.launch_ceiling(mode)
         torch.cuda.synchronize()
         assert torch.equal(sb.buf[:, :k], before[:, :k]), mode  # inputs untouched
@@ -1565,17 +1526,16 @@ def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m,
     (12, 4, 5_592_406 // 64, 2),        # even S
     (10, 4, 1 << 16, 3),                # 16 | S: every shard aligned
 ])
-@pytest.mark.parametrize("how", ["rule", "tune", "realign64-x32", "realign64", "realign64-x8",
-                                 "tri-x32", "tri-g2"])
+@pytest.mark.parametrize("how", ["rule", "tune", "realign-x32", "realign", "realign-tri-x32",
+                                 "tri-x32", "tri-g2", "tri-x8"])
 def test_readall_layout_round_trip(native_lib, k, m, S, batch, how):
     """Upstream Split of an io.ReadAll body (StripeBatch layout "readall": data shards at
     pitch S inside the body, parity in 64-B AllocAligned buffers at a 64-B pitch): encode
     against the oracle on every stripe, then decodes of m data erasures, of erasures with
     Verify rows and of the parity alone restore every byte. how="tune": every plan first
     times each order its kernels offer; otherwise every plan is pinned to that kernel form
-    (rs_plan_set_orders) where its launch offers it: the 64-vector realigning form
-    (REALIGN 5, misaligned inputs with aligned outputs: the encode and the parity-only
-    decode) or the triple loop's unaligned accesses."""
+    (rs_plan_set_orders) where its launch offers it: the realigning kernel (ring or triple
+    loads) or the triple loop's unaligned accesses."""
     import torch
     from callfs_amd import _native as N
     from callfs_amd.device import Plan, StripeBatch
@@ -1588,8 +1548,12 @@ def test_readall_layout_round_trip(native_lib, k, m, S, batch, how):
     def ready(plan, outputs_aligned=True):
         if how == "tune":
             plan.tune(reps=1)
-        elif how != "rule" and not (how.startswith("realign64") and (aligned or not outputs_aligned)):
-            plan.set_orders([how] * int(N.lib.rs_plan_groups(plan.handle)))
+        elif how != "rule":
+            try:
+                plan.set_orders([how] * int(N.lib.rs_plan_groups(plan.handle)))
+            except N.NativeError as e:  # not offered for this launch: the rule's kernel
+                assert e.code == N.RS_E_ARG
+                assert aligned or not how.startswith("realign"), how  # misaligned: offered
         return plan
 
     ready(Plan.for_batch(sb)).launch()

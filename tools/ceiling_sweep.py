@@ -12,7 +12,8 @@ shape spec: k,m,S,stripes[,erase[,layout]]   erase: '-' = encode, 'none' = all p
             base + (b*n + i)*S from an odd base, every shard at its own byte offset when
             S is odd), 'contig' (the same from an aligned base) or 'readall' (Split of an
             io.ReadAll body: data shards at pitch S in page-aligned bodies, parity in
-            64-B AllocAligned buffers; device.StripeBatch)
+            64-B AllocAligned buffers; device.StripeBatch); 'planar:P' / 'pitch:P' set
+            the shard pitch to P bytes
 usage: python tools/ceiling_sweep.py --shape 10,4,1048576,256,5 --shape ... [--tune 1]
 """
 import argparse
@@ -57,7 +58,11 @@ def build(k, m, S, B, layout, dev):
         base = buf.data_ptr() + (1 if layout == "split" else 0)
         ptrs = [base + (b * n + i) * S for b in range(B) for i in range(n)]
         return buf, ptrs
-    sb = StripeBatch(k, m, S, B, dev, layout=layout if layout in ("readall", "planar", "shardmajor") else "pitch")
+    # "planar:P" / "pitch:P": that layout at an explicit shard pitch of P bytes
+    name, _, p = layout.partition(":")
+    sb = StripeBatch(k, m, S, B, dev,
+                     layout=name if name in ("readall", "planar", "shardmajor") else "pitch",
+                     pitch=int(p) if p else None)
     sb.fill_random(0xCA11F5)
     return sb, sb.pointers()
 
