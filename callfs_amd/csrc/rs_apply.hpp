@@ -104,8 +104,15 @@ __device__ __forceinline__ uint32_t word(const uint4& v, int w) {
 //            global_load_dwordx4
 template <int WPE_, int U_, bool NT_LOAD_, bool NT_STORE_, bool PERSIST_, int BS_ = 256,
           int PD_ = 1, int ORD_ = 0, int RING_ = 0, bool NOMATH_ = false, int REALIGN_ = 0,
-          bool SDWA_ = false, int PROBE_ = 0, int VPF_ = 0, int WIX_ = 0>
+          bool SDWA_ = false, int PROBE_ = 0, int VPF_ = 0, int WIX_ = 0, int DMA_ = 0>
 struct Policy {
+  // > 0: input vectors staged through LDS by LDS-DMA (global_load_lds_dwordx4), DMA shards in
+  // flight per wave in a per-wave ring of DMA 1 KiB slots behind the tables, read back by
+  // ds_read_b128 (rs_apply.hpp "LDS-DMA ring"): loads in flight cost LDS, not VGPRs
+  static constexpr int DMA = DMA_;
+  static_assert(DMA_ == 0 || (REALIGN_ == 0 && WIX_ == 0 && RING_ == 0 && !NOMATH_ && !SDWA_ &&
+                              VPF_ == 0 && PROBE_ == 0 && BS_ == 512 && U_ == 1),
+                "DMA: aligned ring-of-three kernel shape only");
   // LDS kernel, R <= 4, plain ring-of-three loop: input shards in triples, each byte
   // position of a triple resolved by four 6-bit lookups into 64-entry tables of 4-byte
   // entries (built in LDS from the nibble tables) instead of six nibble lookups; Verify
@@ -771,6 +778,50 @@ __device__ __forceinline__ void lds_edges(const ApplyArgs& a, cptr<const uint8_t
   if (bad) atomicOr(a.status + static_cast<size_t>(stripe) * a.status_stride, 1);
 }
 
+// ---- LDS-DMA ring (Policy::DMA) --------------------------------------------------------
+// Each wave owns DMA slots of 1 KiB at dma_stage_off(K) + wave * DMA KiB of the block's LDS,
+// behind the tables. Shard i's 64 lane vectors land in slot i % DMA through one
+// global_load_lds_dwordx4 (lane l's 16 B at slot + 16 l; non-temporal), so the loads in flight
+// hold LDS bytes instead of VGPRs; each lane reads its vector back with ds_read_b128 (slot + 16
+// lane: the 64 lanes' reads cover the slot once, no bank conflict). The DMA is issued by inline
+// asm, outside the compiler's vmcnt bookkeeping: issued through the builtin, hipcc waits
+// vmcnt(0) before every ds_read of the kernel (the table lookups included), which would drain
+// the ring at every lookup. The loop counts the DMAs itself (s_waitcnt vmcnt(n): all but the
+// n youngest vector-memory operations done; inside the loop only DMAs are issued), and a slot
+// is reloaded only after its ds_read_b128 has returned (lgkmcnt(0)). A wave reads only its own
+// slots, so no barrier is needed: the DMA's vmcnt completes when its bytes are in LDS.
+__host__ __device__ inline uint32_t dma_stage_off(int K, int RT) {
+  return (static_cast<uint32_t>(K) * 32u * (RT > 8 ? 16u : 8u) + 1023u) & ~1023u;
+}
+// dynamic LDS of a DMA-ring launch (512-thread blocks: 8 waves)
+inline size_t lds_bytes_dma(int K, int RT, int D) {
+  return dma_stage_off(K, RT) + static_cast<size_t>(8 * 1024) * D;
+}
+
+__device__ __forceinline__ void dma16(const uint4* src, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_dst)
+      : "memory");
+}
+
+// s_waitcnt vmcnt(n), n wave-uniform in [0, 7]
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+  }
+}
+
 // Waves per SIMD the LDS kernel may be limited to: 16-byte entries keep 8 b128 reads
 // (32 VGPRs) in flight, which the register allocator only grants below 5 waves.
 template <int RT>
@@ -909,6 +960,37 @@ void rs_apply_lds(ApplyArgs a) {
           x0 = x1;
           x1 = x2;
         }
+      }
+    } else if constexpr (P::DMA > 0) {
+      // LDS-DMA ring (see above): D shards in flight per wave, consumed in order
+      constexpr int D = P::DMA;
+      static_assert(D >= 2 && D <= 8, "vm_wait counts up to 7 younger DMAs");
+      const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const uint32_t ring = __builtin_amdgcn_readfirstlane(lds0 + dma_stage_off(K, RT) + wave * (D * 1024u));
+      const uint32_t mine = ring + lane * 16u;
+      auto src = [&](int i) { return reinterpret_cast<const uint4*>(in[i]) + v0; };
+      auto take = [&](uint32_t slot) {
+        const u32x4 q = *(lds_ptr<u32x4>)(static_cast<uintptr_t>(mine + slot * 1024u));
+        return make_uint4(q.x, q.y, q.z, q.w);
+      };
+      const int npre = K < D ? K : D;
+      for (int i = 0; i < npre; ++i) dma16(src(i), ring + static_cast<uint32_t>(i) * 1024u);
+      uint32_t slot = 0;
+      int i = 0;
+#pragma unroll 1
+      for (; i < K - D; ++i) {  // steady state: D - 1 younger DMAs in flight
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 1) : "memory");
+        const uint4 x = take(slot);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: reload it
+        dma16(src(i + D), ring + slot * 1024u);
+        lds_mac<RT>(acc, x, lds0 + static_cast<uint32_t>(i) * 32u * W);
+        slot = slot + 1 == D ? 0u : slot + 1;
+      }
+#pragma unroll 1
+      for (; i < K; ++i) {  // the last D shards: nothing left to issue
+        vm_wait(K - 1 - i);
+        lds_mac<RT>(acc, take(slot), lds0 + static_cast<uint32_t>(i) * 32u * W);
+        slot = slot + 1 == D ? 0u : slot + 1;
       }
     } else if constexpr (P::WIX == 3 || P::WIX == 5) {
       // groups of G = 3 (WIX 3) or 2 (WIX 5) shards double-buffered in two register sets,

@@ -115,6 +115,12 @@ template <int ORD>
 using LdsRealignTriDbPolicy = dev::Policy<5, 1, true, true, false, 512, 2, ORD, 0, false, 2, false, 0, 0, 3>;
 template <int ORD>
 using LdsRealignOutPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, false, 2>;
+// Input vectors staged through an LDS-DMA ring of kDmaDepth shards per wave (rs_apply.hpp
+// Policy::DMA): R <= 8, aligned shards, at most 64 KiB of LDS (K <= 64); A/B build
+constexpr int kDmaDepth = 6;
+template <int R, int ORD>
+using LdsDmaPolicy = dev::Policy<(R <= 4 ? 8 : 6), 1, true, true, false, 512, 2, ORD, 0, false, 0,
+                                 false, 0, 0, 0, kDmaDepth>;
 template <int ORD>
 using LdsRealignOut8Policy = dev::Policy<8, 1, true, true, false, 512, 2, ORD, 0, false, 2>;
 template <int R, int ORD>
@@ -339,6 +345,28 @@ const std::array<std::array<VecFn, 4>, 5> kLdsTriVerify = {
 template <int ORD, int... Rs>
 constexpr auto lds_realign_tri_table(std::integer_sequence<int, Rs...>) {
   return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsRealignTriPolicy<Rs + 1, ORD>>...};
+}
+#if CALLFS_RS_AB_INSTANCES
+template <int ORD, int... Rs>
+constexpr auto lds_dma_table(std::integer_sequence<int, Rs...>) {
+  return std::array<VecFn, sizeof...(Rs)>{&dev::rs_apply_lds<Rs + 1, LdsDmaPolicy<Rs + 1, ORD>>...};
+}
+// [consecutive, G2, Q8, X32][R - 1] (A/B build)
+const std::array<std::array<VecFn, 8>, 4> kLdsDma = {
+    lds_dma_table<0>(std::make_integer_sequence<int, 8>{}), lds_dma_table<5>(std::make_integer_sequence<int, 8>{}),
+    lds_dma_table<6>(std::make_integer_sequence<int, 8>{}), lds_dma_table<11>(std::make_integer_sequence<int, 8>{})};
+int dma_index(TileOrder o) {
+  switch (o) {
+    case TileOrder::kGroup2: return 1;
+    case TileOrder::kSeg8: return 2;
+    case TileOrder::kXcd32: return 3;
+    default: return 0;
+  }
+}
+#endif
+bool can_dma(const ApplyArgs& a) {
+  return kAbInstances && a.R <= 8 && a.K >= 2 && !(a.in_misalign | a.out_misalign) &&
+         dev::lds_bytes_dma(a.K, a.R, kDmaDepth) <= (64u << 10);
 }
 #if CALLFS_RS_AB_INSTANCES
 // [consecutive, X8, X32][R - 1], R <= 4 (A/B build)
@@ -648,6 +676,10 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       if (tps > 1024 || (every_instance && tps >= 64)) add(tri_in(TileOrder::kSeg16));
       if (tps > 1024 || every_instance) add(tri_in(TileOrder::kXcd8));
     }
+    if (every_instance && can_dma(a)) {  // the LDS-DMA ring: A/B build only
+      for (TileOrder o : {TileOrder::kConsecutive, TileOrder::kGroup2, TileOrder::kSeg8, TileOrder::kXcd32})
+        add(static_cast<TileOrder>(kOrderDma + static_cast<int>(o)));
+    }
     if (kAbInstances && every_instance && can_wix(a)) {  // WIX: A/B build only
       const int n0 = static_cast<int>(c.size());
       for (int i = 0; i < n0; ++i)
@@ -667,6 +699,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
+  const bool dma = order >= kOrderDma && can_dma(a);
+  if (order >= kOrderDma) order = dma ? order - kOrderDma : -1;
   // realigning kernel with triple loads: kOrderRealignTri + its order -> kOrderRealign + it
   const bool r64 = order >= kOrderRealign64 && can_realign64(a);
   if (order >= kOrderRealign64) order = r64 ? order - kOrderRealign64 + kOrderRealign : -1;
@@ -726,6 +760,12 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
             else
               fn = kLdsTri[ti][a.R - 1];
           }
+#if CALLFS_RS_AB_INSTANCES
+          if (dma) {
+            fn = kLdsDma[dma_index(ord)][a.R - 1];
+            lds = dev::lds_bytes_dma(a.K, a.R, kDmaDepth);
+          }
+#endif
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
         }
@@ -757,7 +797,8 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
                           LdsVerifyPolicy<0>::BS == LdsPolicy::BS &&
                           LdsWixPolicy<0>::TILE_VECS == LdsPolicy::TILE_VECS &&
                           LdsWidePolicy::TILE_VECS == LdsPolicy::TILE_VECS &&
-                          LdsWideQ8Policy::TILE_VECS == LdsPolicy::TILE_VECS,
+                          LdsWideQ8Policy::TILE_VECS == LdsPolicy::TILE_VECS &&
+                          LdsDmaPolicy<8, 0>::TILE_VECS == LdsPolicy::TILE_VECS,
                       "one grid shape and tail placement (tail_code) for every LDS policy");
         unsigned gx = dev::vec_grid<LdsPolicy>(a.nvec, a.batch);
         // misaligned shards: the realigning form, unless a tuned order names a plain kernel

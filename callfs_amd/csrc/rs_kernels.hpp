@@ -131,6 +131,9 @@ constexpr int kOrderRealignTri = 128;
 // one extra single-lane load, stores unshifted in 1 KiB wave windows; rs_apply.hpp
 // REALIGN 5)
 constexpr int kOrderRealign64 = 160;
+// (kOrderDma + consecutive / G2 / Q8 / X32: aligned R <= 8 launches with their input vectors
+// staged through an LDS-DMA ring, rs_apply.hpp Policy::DMA; A/B build)
+constexpr int kOrderDma = 192;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the

@@ -97,6 +97,59 @@ func decodeErr(rc C.int) error {
 	return fmt.Errorf("erasure: reconstruction failed: %w", upstreamErr(rc))
 }
 
+// ---- pinned host buffers (zero-copy bodies) -------------------------------------------
+//
+// HostBuffer / BodyBuffer hand out page-locked host memory from rs_host_alloc as Go byte
+// slices (C memory: cgo's pointer rules and runtime.Pinner do not apply to it, and the GC
+// never moves it). When every shard of a call lies inside such buffers, the library runs
+// the call zero-copy: H2D, kernels and D2H straight on these bytes, no CPU copy through its
+// staging (include/callfs_rs.h rs_host_alloc; DESIGN.md §6.3, 38-45 GiB/s for objects of
+// 10 MiB and up on one request thread). Upload bodies read into a BodyBuffer instead of
+// io.ReadAll's heap slice (post_file_enhanced.go:125-127) and shards fetched into
+// HostBuffers instead of io.ReadAll (manager.go:473,530) take that path. Release each with
+// FreeHostBuffer; the context keeps freed buffers and hands them to later requests of a
+// similar size (2 MiB granules), so page-locking is paid once, not per request.
+
+// HostBuffer returns n bytes of pinned host memory, or nil when there is no device (read
+// into a heap buffer then, as before).
+func HostBuffer(n int) []byte {
+	if n <= 0 || device() == nil {
+		return nil
+	}
+	var p unsafe.Pointer
+	if C.rs_host_alloc(gpuCtx, C.size_t(n), &p) != C.RS_OK {
+		return nil
+	}
+	return unsafe.Slice((*byte)(p), n)
+}
+
+// BodyBuffer returns a pinned buffer of length size with capacity for the profile's n
+// shards, n * ceil(size/k) bytes: read the upload body into it and pass it to Encode,
+// whose Split (split below, as upstream's codec.go:31) then lays the data shards and the
+// parity inside the one pinned allocation. nil when there is no device or the profile
+// takes the CPU codec (k+m > 256).
+func BodyBuffer(size int, profile ErasureProfile) []byte {
+	k, m := profile.DataShards, profile.ParityShards
+	if k < 1 || m < 1 || k+m > 256 || size <= 0 {
+		return nil
+	}
+	S := (size + k - 1) / k
+	b := HostBuffer((k + m) * S)
+	if b == nil {
+		return nil
+	}
+	return b[:size]
+}
+
+// FreeHostBuffer releases a HostBuffer or BodyBuffer (any reslice of it that starts at its
+// first byte). A nil or heap slice is ignored.
+func FreeHostBuffer(b []byte) {
+	if cap(b) == 0 || gpuCtx == nil {
+		return
+	}
+	C.rs_host_free(gpuCtx, unsafe.Pointer(unsafe.SliceData(b)))
+}
+
 // cArray is n pointer-sized C slots (cgo: a Go []*T passed to C may not hold Go
 // pointers; a C array may, while each pointee is pinned).
 type cArray struct {
@@ -186,6 +239,20 @@ func split(data []byte, k, m int) [][]byte {
 // ErrTooFewShards / ErrShardSize / ErrShardNoData leaves the caller's slice exactly as
 // it was (codec_test.go:65-88).
 func (c *Codec) Decode(shards [][]byte, profile ErasureProfile, originalSize int64) ([]byte, error) {
+	return c.decode(shards, profile, originalSize, false)
+}
+
+// DecodePinned is Decode for shards fetched into HostBuffers (manager.go:473,530 reading
+// into HostBuffer(S) instead of io.ReadAll): the reconstructed entries it fills and the
+// object it returns are HostBuffers too, so the whole call runs zero-copy. The caller
+// releases the returned object and every shard entry with FreeHostBuffer once the response
+// is written. Without a device it is Decode (heap buffers, FreeHostBuffer ignores them).
+// Not in the reference API: an addition for servers that read into pinned buffers.
+func (c *Codec) DecodePinned(shards [][]byte, profile ErasureProfile, originalSize int64) ([]byte, error) {
+	return c.decode(shards, profile, originalSize, true)
+}
+
+func (c *Codec) decode(shards [][]byte, profile ErasureProfile, originalSize int64, pinned bool) ([]byte, error) {
 	k, m := profile.DataShards, profile.ParityShards
 	if k < 1 || m < 1 {
 		return nil, ErrInvalidProfile
@@ -193,6 +260,17 @@ func (c *Codec) Decode(shards [][]byte, profile ErasureProfile, originalSize int
 	n := k + m
 	if n > 256 || originalSize < int64(gpuMinBytes) || device() == nil {
 		return c.cpuDecode(shards, profile, originalSize)
+	}
+	alloc := func(size int) []byte { return make([]byte, size) }
+	var owned [][]byte // HostBuffers this call allocated, released unless handed over
+	if pinned {
+		alloc = func(size int) []byte {
+			if b := HostBuffer(size); b != nil {
+				owned = append(owned, b)
+				return b
+			}
+			return make([]byte, size)
+		}
 	}
 	if len(shards) != n {
 		return nil, fmt.Errorf("erasure: reconstruction failed: %w", reedsolomon.ErrTooFewShards)
@@ -221,7 +299,7 @@ func (c *Codec) Decode(shards [][]byte, profile ErasureProfile, originalSize int
 			if cap(bufs[i]) >= S {
 				bufs[i] = bufs[i][:S]
 			} else {
-				bufs[i] = make([]byte, S)
+				bufs[i] = alloc(S)
 			}
 		}
 		if len(bufs[i]) > 0 {
@@ -229,20 +307,30 @@ func (c *Codec) Decode(shards [][]byte, profile ErasureProfile, originalSize int
 			ptrs.set(i, unsafe.Pointer(&bufs[i][0]))
 		}
 	}
-	buf := make([]byte, originalSize)
+	buf := alloc(int(originalSize))
 	var out *C.uint8_t
 	if originalSize > 0 {
 		pin.Pin(&buf[0])
 		out = (*C.uint8_t)(unsafe.Pointer(&buf[0]))
 	}
 	rc := C.rs_codec_decode(gpuCtx, C.int(k), C.int(m), ptrs.at(0), lens, out, C.int64_t(originalSize))
+	handed := map[*byte]bool{}
 	switch rc {
 	case C.RS_OK, C.RS_E_CORRUPT, C.RS_E_INSUFFICIENT:
 		// Reconstruct ran: upstream has filled the nil entries by now (codec.go:55)
 		for i := range shards {
 			if len(shards[i]) == 0 {
 				shards[i] = bufs[i]
+				handed[unsafe.SliceData(bufs[i])] = true
 			}
+		}
+	}
+	if rc == C.RS_OK {
+		handed[unsafe.SliceData(buf)] = true
+	}
+	for _, b := range owned { // pinned buffers the caller did not receive
+		if !handed[unsafe.SliceData(b)] {
+			FreeHostBuffer(b)
 		}
 	}
 	if rc != C.RS_OK {

@@ -192,3 +192,55 @@ func TestGPURepairBatch(t *testing.T) {
 		}
 	}
 }
+
+// BodyBuffer / HostBuffer / DecodePinned: an upload body read into a pinned BodyBuffer
+// encodes in place (every shard inside the one allocation, zero-copy) to reedsolomon's
+// bytes; shards fetched into HostBuffers decode through DecodePinned; freed buffers are
+// reused by the next request of the same size. tests/native/cgo_drive.c runs the same
+// contract through the C ABI.
+func TestGPUPinnedBodies(t *testing.T) {
+	withGPU(t)
+	c := NewCodec()
+	p := ErasureProfile{DataShards: 10, ParityShards: 4}
+	const size = 10<<20 + 3
+	for round := 0; round < 2; round++ {
+		body := BodyBuffer(size, p)
+		if body == nil || len(body) != size || cap(body) != 14*((size+9)/10) {
+			t.Fatalf("BodyBuffer: len %d cap %d", len(body), cap(body))
+		}
+		copy(body, randBytes(int64(round+7), size))
+		want, err := c.cpuEncode(append([]byte(nil), body...), p)
+		if err != nil {
+			t.Fatal(err)
+		}
+		shards, err := c.Encode(body, p)
+		if err != nil {
+			t.Fatal(err)
+		}
+		fetched := make([][]byte, len(shards))
+		for i := range shards {
+			if !bytes.Equal(shards[i], want[i]) {
+				t.Fatalf("round %d: shard %d differs from reedsolomon", round, i)
+			}
+			if i%4 != 1 { // three data shards and a parity shard lost
+				fetched[i] = HostBuffer(len(shards[i]))
+				copy(fetched[i], shards[i])
+			}
+		}
+		FreeHostBuffer(body)
+		got, err := c.DecodePinned(fetched, p, size)
+		if err != nil {
+			t.Fatal(err)
+		}
+		if !bytes.Equal(got, bytes.Join(want[:10], nil)[:size]) {
+			t.Fatalf("round %d: DecodePinned object differs", round)
+		}
+		for i := range fetched {
+			if !bytes.Equal(fetched[i], want[i]) {
+				t.Fatalf("round %d: entry %d not reconstructed", round, i)
+			}
+			FreeHostBuffer(fetched[i])
+		}
+		FreeHostBuffer(got)
+	}
+}

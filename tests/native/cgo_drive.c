@@ -171,6 +171,16 @@ static void argument_paths(rs_ctx* ctx, int k, int m, size_t S, uint8_t* const* 
     CHECK(rs_codec_encode(ctx, 0, m, buf, 1, buf, 8, &ss) == RS_E_INVALID_PROFILE);
     CHECK(ss == 7); /* not written on error */
   }
+  /* pinned host buffers (the shim's HostBuffer / BodyBuffer / FreeHostBuffer): bad
+     arguments return before the context is touched */
+  {
+    void* p = (void*)0x1;
+    CHECK(rs_host_alloc(NULL, 16, &p) == RS_E_ARG);
+    CHECK(rs_host_alloc(ctx, 0, &p) == RS_E_ARG);
+    CHECK(rs_host_alloc(ctx, 16, NULL) == RS_E_ARG);
+    CHECK(rs_host_free(NULL, out) == RS_E_ARG);
+    CHECK(rs_host_free(ctx, NULL) == RS_E_ARG);
+  }
   free(miss);
 }
 
@@ -244,6 +254,63 @@ static void device_paths(rs_ctx* ctx, int k, int m, size_t L) {
   free(all); free(data);
 }
 
+/* The shim's pinned-body contract (codec_rocm.go BodyBuffer, Encode, DecodePinned,
+ * FreeHostBuffer): allocate a body with room for all n shards, fill it, Split in place
+ * (zero padding past L), encode with every shard inside the one allocation (zero-copy);
+ * decode from shards fetched into host buffers into host buffers; free everything; the
+ * next request of the same size gets the freed body back from the context's pool. */
+static void host_body_paths(rs_ctx* ctx, int k, int m, size_t L, int same_body) {
+  const int n = k + m;
+  const size_t S = (L + (size_t)k - 1) / (size_t)k;
+  void* first = NULL;
+  for (int round = 0; round < 2; round++) {
+    uint8_t* body = NULL;
+    CHECK(rs_host_alloc(ctx, S * (size_t)n, (void**)&body) == RS_OK && body != NULL);
+    if (!body) return;
+    if (round == 0) first = body;
+    else if (same_body) CHECK((void*)body == first); /* the freed body came back (the only
+                                                         kept buffer of its size class) */
+    uint32_t seed = (uint32_t)(L + 17u * (unsigned)round);
+    for (size_t i = 0; i < L; i++) body[i] = (uint8_t)lcg(&seed);
+    memset(body + L, 0, S * (size_t)n - L); /* Split zeroes the spare capacity */
+    const uint8_t** din = (const uint8_t**)malloc(sizeof(uint8_t*) * (size_t)k);
+    uint8_t** pout = (uint8_t**)malloc(sizeof(uint8_t*) * (size_t)m);
+    uint8_t* want = (uint8_t*)malloc(S * (size_t)m);
+    for (int i = 0; i < k; i++) din[i] = body + S * (size_t)i;
+    for (int j = 0; j < m; j++) pout[j] = body + S * (size_t)(k + j);
+    CHECK(rs_encode(ctx, k, m, S, din, pout) == RS_OK);
+    for (int j = 0; j < m; j++) pout[j] = want + S * (size_t)j;
+    CHECK(orc_encode(k, m, S, din, pout) == 0);
+    CHECK(memcmp(body + S * (size_t)k, want, S * (size_t)m) == 0);
+    /* DecodePinned: fetched shards, the reconstructed entries and the object pinned too */
+    uint8_t** sh = (uint8_t**)malloc(sizeof(uint8_t*) * (size_t)n);
+    size_t* lens = (size_t*)malloc(sizeof(size_t) * (size_t)n);
+    for (int i = 0; i < n; i++) {
+      CHECK(rs_host_alloc(ctx, S, (void**)&sh[i]) == RS_OK);
+      if (i % 4 == 1) {
+        memset(sh[i], SENTINEL, S);
+        lens[i] = 0;
+      } else {
+        memcpy(sh[i], body + S * (size_t)i, S);
+        lens[i] = S;
+      }
+    }
+    uint8_t* out = NULL;
+    CHECK(rs_host_alloc(ctx, L, (void**)&out) == RS_OK);
+    CHECK(rs_codec_decode(ctx, k, m, sh, lens, out, (int64_t)L) == RS_OK);
+    CHECK(memcmp(out, body, L) == 0);
+    for (int i = 0; i < n; i++) {
+      CHECK(lens[i] == S && memcmp(sh[i], body + S * (size_t)i, S) == 0);
+      CHECK(rs_host_free(ctx, sh[i]) == RS_OK);
+    }
+    CHECK(rs_host_free(ctx, out) == RS_OK);
+    CHECK(rs_host_free(ctx, body) == RS_OK);
+    CHECK(rs_host_free(ctx, body) == RS_E_ARG); /* already freed */
+    CHECK(rs_host_free(ctx, want) == RS_E_ARG); /* not rs_host_alloc memory */
+    free(lens); free(sh); free(want); free(pout); free(din);
+  }
+}
+
 int main(int argc, char** argv) {
   const int need_gpu = argc > 1 && strcmp(argv[1], "gpu") == 0;
   rs_ctx* ctx = NULL;
@@ -271,6 +338,8 @@ int main(int argc, char** argv) {
   device_paths(ctx, 10, 4, (1u << 20) + 7);  /* ragged tail */
   device_paths(ctx, 4, 2, 3u << 20);         /* RS(4,2) 1 MiB shards */
   device_paths(ctx, 16, 4, 64u << 20);       /* pipeline with several chunks */
+  host_body_paths(ctx, 10, 4, (10u << 20) + 3, 1); /* pinned bodies, zero-copy */
+  host_body_paths(ctx, 4, 2, 4096, 0);             /* a small body: the one-dispatch path */
   rs_shutdown(ctx);
   printf(fails ? "cgo_drive FAILED (%d)\n" : "cgo_drive ok (device round trips)\n", fails);
   return fails != 0;

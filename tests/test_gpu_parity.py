@@ -1226,7 +1226,8 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
 ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign",
                    "realign-x8", "realign-x32", "wix", "wix-g8", "wix-g2", "wix-q8", "wix-q16",
                    "wix-x8", "wix-x32", "tri", "tri-g2", "tri-x32", "tri-q8", "tri-q16",
-                   "tri-x8", "realign-tri", "realign-tri-x8", "realign-tri-x32"]
+                   "tri-x8", "realign-tri", "realign-tri-x8", "realign-tri-x32",
+                   "dma", "dma-g2", "dma-q8", "dma-x32"]
 
 
 @pytest.mark.parametrize("k,m,S,batch,off,erase", [
@@ -1293,8 +1294,11 @@ def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, era
         assert {"x8", "x32"} <= set(taken), taken
         with pytest.raises(N.NativeError):
             plan.set_orders(["realign"])  # aligned shards: no realigning kernel
-    # the 6-bit triple lookups (Policy::WIX 1) are A/B-build forms: the product refuses them
-    assert not any(t.startswith("wix") for t in taken), taken
+    # the 6-bit triple lookups (Policy::WIX 1) and the LDS-DMA ring are A/B-build forms: the
+    # product refuses them (run with CALLFS_RS_LIB=callfs_amd/libcallfs_rs_ab.so, the A/B
+    # build offers and checks them here)
+    if "libcallfs_rs_ab" not in N.LIB_PATH:
+        assert not any(t.startswith(("wix", "dma")) for t in taken), taken
     with pytest.raises(N.NativeError):
         plan.set_orders(["none"] * (plan_groups := int(N.lib.rs_plan_groups(plan.handle))) + ["none"])
     plan.set_orders(["none"] * plan_groups)
