@@ -85,6 +85,13 @@ def main():
         erase = f[4] if len(f) > 4 else "-"
         layout = f[5] if len(f) > 5 else "pitch"
         n = k + m
+        if erase not in ("-", "none") and (len({int(x) for x in erase.split("+")}) > m or
+                                           max(int(x) for x in erase.split("+")) >= n):
+            # (round 4's layout probe asked for 3 erasures of RS(4,2) and died in
+            # rs_plan_create: an unrecoverable shape is reported, not run)
+            print(json.dumps({"shape": spec, "skipped": f"erase {erase} is not recoverable "
+                                                        f"for RS({k},{m})"}), flush=True)
+            continue
         holder, ptrs = build(k, m, S, B, layout, dev)
         enc = Plan(k, m, S, B, ptrs)
         enc.launch(stream)
