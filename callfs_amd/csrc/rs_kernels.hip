@@ -650,7 +650,7 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
     }
     add(TileOrder::kConsecutive);
     add(TileOrder::kGroup2);
-    if (tps <= 32) add(TileOrder::kGroup8);
+    if (tps <= 32 || every_instance) add(TileOrder::kGroup8);
     // Q8 from 64 tiles per stripe (8 segments of >= 8 tiles): at 1 MiB shards it ran within
     // a point of the best order and ahead of the rule's on some boxes (RS(16,4) 77.7 vs 76.8,
     // profiles/r04/tri_sweep1); Q16 above 8 MiB as before

@@ -1,0 +1,147 @@
+// Write-stream pattern probe (development tool, not product): what HBM serves best for the
+// parity writes of long shards. Every block (512 threads, one 16-B store per lane per row)
+// writes an 8 KiB tile of each of R rows; rows sit `pitch` bytes apart, stripes of R rows
+// back to back (the planar parity region). Tile order: block b -> (stripe, tile) as
+// consecutive (a stripe's tiles in order), G-interleaved (the same tile of G stripes on
+// neighbouring blocks) or Q-segmented. Also a pure linear write of the same byte count.
+// Prints GB/s per variant, best of `reps` launches, after a warm-up.
+//
+// build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/write_pattern.hip -o tools/write_pattern
+// run:   tools/write_pattern [reps]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                                  \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) {                                                                    \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));          \
+      std::exit(1);                                                                            \
+    }                                                                                          \
+  } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct Args {
+  uint8_t* base;
+  uint64_t pitch;   // bytes between rows
+  uint32_t R;       // rows per stripe
+  uint32_t tps;     // tiles per row
+  uint32_t batch;   // stripes
+  uint32_t order;   // 0 consecutive, 1 G-interleave, 2 Q-segments, 3 linear
+  uint32_t g;       // G or Q
+  uint32_t read;    // 1: read the same bytes instead of writing them
+  uint32_t rowwave; // 1: a wave's R stores go to consecutive 1 KiB pieces of one row (the
+                    // block's 8R pieces dealt wave-major) instead of one piece of each row;
+                    // 2: one piece of each row, each store waited for before the next
+  uint32_t* sink;
+};
+
+__global__ __launch_bounds__(512) void pattern(Args a) {
+  const uint32_t t = blockIdx.x;
+  uint32_t stripe, tile;
+  if (a.order == 1) {
+    const uint32_t per = a.g * a.tps, grp = t / per, r = t - grp * per;
+    const uint32_t gsz = min(a.g, a.batch - grp * a.g);
+    tile = r / gsz;
+    stripe = grp * a.g + (r - tile * gsz);
+  } else if (a.order == 2) {
+    stripe = t / a.tps;
+    const uint32_t r = t - stripe * a.tps, seg = a.tps / a.g;
+    tile = r < seg * a.g ? (r % a.g) * seg + r / a.g : r;
+  } else {
+    stripe = t / a.tps;
+    tile = t - stripe * a.tps;
+  }
+  const uint32_t x = t * 0x9E3779B1u + threadIdx.x;
+  u32x4 acc = {0, 0, 0, 0};
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t i = 0; i < a.R; ++i) {
+    // piece f of the block's 8R 1 KiB pieces: row f / 8, piece f % 8 of the row's 8 KiB tile
+    const uint32_t f = a.rowwave ? w * a.R + i : i * 8 + w;
+    const uint32_t r = f / 8, piece = f % 8;
+    uint8_t* row = a.order == 3
+                       ? a.base + (static_cast<uint64_t>(t) * a.R + r) * 8192
+                       : a.base + (static_cast<uint64_t>(stripe) * a.R + r) * a.pitch +
+                             static_cast<uint64_t>(tile) * 8192;
+    u32x4* p = reinterpret_cast<u32x4*>(row + piece * 1024) + lane;
+    if (a.read) {
+      acc ^= __builtin_nontemporal_load(p);
+    } else {
+      const u32x4 v = {x, x + r, x ^ r, r};
+      __builtin_nontemporal_store(v, p);
+      if (a.rowwave == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // one store in flight
+    }
+  }
+  if (a.read && acc.x == 0x12345678u && acc.y == 0x9abcdef0u) a.sink[0] = acc.z;
+}
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? std::atoi(argv[1]) : 10;
+  const uint64_t total = 6ull << 30;  // bytes written per launch (approximately)
+  uint8_t* buf;
+  CK(hipMalloc(&buf, total + (64ull << 20)));
+  uint32_t* sink;
+  CK(hipMalloc(&sink, 64));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  struct V {
+    const char* name;
+    uint64_t S;
+    uint32_t R, order, g, read, rowwave;
+  };
+  std::vector<V> vs;
+  const uint64_t shapes[] = {1ull << 20, 2ull << 20, 6710912, 8ull << 20, 64ull << 20};
+  for (uint32_t rw = 0; rw < 3; rw += 2)
+    for (uint64_t S : shapes)
+      for (uint32_t R : {4u, 8u}) {
+        vs.push_back({rw ? "consecutive-ser" : "consecutive", S, R, 0, 0, 0, rw});
+        vs.push_back({rw ? "G2-ser" : "G2", S, R, 1, 2, 0, rw});
+        vs.push_back({rw ? "G8-ser" : "G8", S, R, 1, 8, 0, rw});
+        vs.push_back({rw ? "Q8-ser" : "Q8", S, R, 2, 8, 0, rw});
+      }
+  vs.push_back({"linear", 8192, 4, 3, 0, 0, 0});
+  vs.push_back({"linear-ser", 8192, 4, 3, 0, 0, 2});
+  vs.push_back({"linear", 8192, 1, 3, 0, 0, 0});
+  std::printf("variant,shard_bytes,rows,mode,GBps\n");
+  for (const V& v : vs) {
+    Args a{};
+    a.base = buf;
+    a.pitch = v.S;
+    a.R = v.R;
+    a.tps = static_cast<uint32_t>(v.S / 8192);
+    a.batch = static_cast<uint32_t>(total / (v.S * v.R));
+    a.order = v.order;
+    a.g = v.g;
+    a.read = v.read;
+    a.rowwave = v.rowwave;
+    a.sink = sink;
+    uint32_t grid = a.tps * a.batch;
+    if (v.order == 3) {
+      a.tps = 1;
+      grid = static_cast<uint32_t>(total / (8192ull * v.R));
+      a.batch = grid;
+    }
+    const double bytes = static_cast<double>(grid) * v.R * 8192;
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(pattern, dim3(grid), dim3(512), 0, 0, a);
+    float best = 1e30f;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0));
+      hipLaunchKernelGGL(pattern, dim3(grid), dim3(512), 0, 0, a);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best;
+    }
+    std::printf("%s,%llu,%u,%s,%.0f\n", v.name, static_cast<unsigned long long>(v.S), v.R,
+                v.read ? "read" : "write", bytes / (best * 1e-3) / 1e9);
+    std::fflush(stdout);
+  }
+  CK(hipFree(buf));
+  return 0;
+}
