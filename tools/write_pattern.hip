@@ -40,7 +40,7 @@ struct Args {
   uint32_t* sink;
 };
 
-__global__ __launch_bounds__(512) void pattern(Args a) {
+__global__ __launch_bounds__(1024) void pattern(Args a) {
   const uint32_t t = blockIdx.x;
   uint32_t stripe, tile;
   if (a.order == 1) {
@@ -58,15 +58,16 @@ __global__ __launch_bounds__(512) void pattern(Args a) {
   }
   const uint32_t x = t * 0x9E3779B1u + threadIdx.x;
   u32x4 acc = {0, 0, 0, 0};
-  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const uint64_t tb = blockDim.x * 16ull;  // tile bytes per row
   for (uint32_t i = 0; i < a.R; ++i) {
-    // piece f of the block's 8R 1 KiB pieces: row f / 8, piece f % 8 of the row's 8 KiB tile
-    const uint32_t f = a.rowwave ? w * a.R + i : i * 8 + w;
-    const uint32_t r = f / 8, piece = f % 8;
+    // piece f of the block's nw*R 1 KiB pieces: row f / nw, piece f % nw of the row's tile
+    const uint32_t f = a.rowwave ? w * a.R + i : i * nw + w;
+    const uint32_t r = f / nw, piece = f % nw;
     uint8_t* row = a.order == 3
-                       ? a.base + (static_cast<uint64_t>(t) * a.R + r) * 8192
+                       ? a.base + (static_cast<uint64_t>(t) * a.R + r) * tb
                        : a.base + (static_cast<uint64_t>(stripe) * a.R + r) * a.pitch +
-                             static_cast<uint64_t>(tile) * 8192;
+                             static_cast<uint64_t>(tile) * tb;
     u32x4* p = reinterpret_cast<u32x4*>(row + piece * 1024) + lane;
     if (a.read) {
       acc ^= __builtin_nontemporal_load(p);
@@ -92,28 +93,25 @@ int main(int argc, char** argv) {
   struct V {
     const char* name;
     uint64_t S;
-    uint32_t R, order, g, read, rowwave;
+    uint32_t R, order, g, read, rowwave, bs;
   };
   std::vector<V> vs;
   const uint64_t shapes[] = {1ull << 20, 2ull << 20, 6710912, 8ull << 20, 64ull << 20};
-  for (uint32_t rw = 0; rw < 3; rw += 2)
+  for (uint32_t bs : {128u, 256u, 512u, 1024u})
     for (uint64_t S : shapes)
-      for (uint32_t R : {4u, 8u}) {
-        vs.push_back({rw ? "consecutive-ser" : "consecutive", S, R, 0, 0, 0, rw});
-        vs.push_back({rw ? "G2-ser" : "G2", S, R, 1, 2, 0, rw});
-        vs.push_back({rw ? "G8-ser" : "G8", S, R, 1, 8, 0, rw});
-        vs.push_back({rw ? "Q8-ser" : "Q8", S, R, 2, 8, 0, rw});
+      for (uint32_t R : {1u, 4u, 8u}) {
+        vs.push_back({"consecutive", S, R, 0, 0, 0, 0, bs});
+        vs.push_back({"G8", S, R, 1, 8, 0, 0, bs});
+        vs.push_back({"Q8", S, R, 2, 8, 0, 0, bs});
       }
-  vs.push_back({"linear", 8192, 4, 3, 0, 0, 0});
-  vs.push_back({"linear-ser", 8192, 4, 3, 0, 0, 2});
-  vs.push_back({"linear", 8192, 1, 3, 0, 0, 0});
-  std::printf("variant,shard_bytes,rows,mode,GBps\n");
+  std::printf("variant,shard_bytes,rows,block,mode,GBps\n");
   for (const V& v : vs) {
     Args a{};
     a.base = buf;
     a.pitch = v.S;
     a.R = v.R;
-    a.tps = static_cast<uint32_t>(v.S / 8192);
+    const uint64_t tb = v.bs * 16ull;
+    a.tps = static_cast<uint32_t>(v.S / tb);
     a.batch = static_cast<uint32_t>(total / (v.S * v.R));
     a.order = v.order;
     a.g = v.g;
@@ -123,23 +121,23 @@ int main(int argc, char** argv) {
     uint32_t grid = a.tps * a.batch;
     if (v.order == 3) {
       a.tps = 1;
-      grid = static_cast<uint32_t>(total / (8192ull * v.R));
+      grid = static_cast<uint32_t>(total / (tb * v.R));
       a.batch = grid;
     }
-    const double bytes = static_cast<double>(grid) * v.R * 8192;
-    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(pattern, dim3(grid), dim3(512), 0, 0, a);
+    const double bytes = static_cast<double>(grid) * v.R * tb;
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(pattern, dim3(grid), dim3(v.bs), 0, 0, a);
     float best = 1e30f;
     for (int r = 0; r < reps; ++r) {
       CK(hipEventRecord(e0));
-      hipLaunchKernelGGL(pattern, dim3(grid), dim3(512), 0, 0, a);
+      hipLaunchKernelGGL(pattern, dim3(grid), dim3(v.bs), 0, 0, a);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       best = ms < best ? ms : best;
     }
-    std::printf("%s,%llu,%u,%s,%.0f\n", v.name, static_cast<unsigned long long>(v.S), v.R,
-                v.read ? "read" : "write", bytes / (best * 1e-3) / 1e9);
+    std::printf("%s,%llu,%u,%u,%s,%.0f\n", v.name, static_cast<unsigned long long>(v.S), v.R,
+                v.bs, v.read ? "read" : "write", bytes / (best * 1e-3) / 1e9);
     std::fflush(stdout);
   }
   CK(hipFree(buf));
