@@ -50,3 +50,26 @@ def test_planar_layout_separates_data_and_parity():
     par = sorted(p[b * (k + m) + k + j] for b in range(4) for j in range(m))
     assert all(x % 256 == 0 for x in data + par)
     assert data[-1] + S <= par[0] or par[-1] + S <= data[0]  # two disjoint regions
+
+
+@pytest.mark.parametrize("layout", ["planar", "pitch", "shardmajor"])
+def test_explicit_pitch(layout):
+    """StripeBatch(pitch=P) (bench.py --pitch, tools/pitch_sweep.sh): every shard at that
+    pitch within its region; a pitch below S, not a multiple of 16, or for an upstream Split
+    layout is refused."""
+    k, m, S, P = 10, 4, 6_710_887 // 64, 6_710_887 // 64 + 4096 + 9
+    P -= P % 16
+    sb = StripeBatch(k, m, S, 3, torch.device("cpu"), layout=layout, pitch=P)
+    assert sb.pitch == P
+    p = sb.pointers()
+    for b in range(3):
+        assert [p[b * (k + m) + i + 1] - p[b * (k + m) + i] for i in range(k - 1)] == [
+            P if layout != "shardmajor" else 3 * P] * (k - 1)
+    sb.fill_random(1)
+    assert sb.gather().shape == (3, k + m, S)
+    for bad in (S - 16, P + 8):
+        with pytest.raises(ValueError):
+            StripeBatch(k, m, S, 1, torch.device("cpu"), layout=layout, pitch=bad)
+    for split in ("split", "readall"):
+        with pytest.raises(ValueError):
+            StripeBatch(k, m, S, 1, torch.device("cpu"), layout=split, pitch=P)
