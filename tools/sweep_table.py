@@ -9,6 +9,9 @@ for path in sys.argv[1:]:
         if not ln.startswith("{"):
             continue
         r = json.loads(ln)
+        if "skipped" in r:
+            print(f"{r['shape']}: skipped ({r['skipped']})")
+            continue
         p = r["pct_of_8TBs"]
         print(f"{r['k']:>3},{r['m']:<2} S={r['S']:>10} {r['erase']:>9} {r['layout']:>22} "
               f"prod {p.get('prod', 0):6.2f} tuned {p.get('tuned', 0):6.2f} "
