@@ -363,7 +363,16 @@ int dma_index(TileOrder o) {
     default: return 0;
   }
 }
+// [G4, G8][R - 1]: the double-buffered triples with 4 / 8 stripes interleaved (A/B build)
+const std::array<std::array<VecFn, 4>, 2> kLdsTriDbG = {
+    lds_order_table<LdsTriDbPolicy<4>>(std::make_integer_sequence<int, 4>{}),
+    lds_order_table<LdsTriDbPolicy<2>>(std::make_integer_sequence<int, 4>{})};
 #endif
+bool can_tridb_g(const ApplyArgs& a) {
+  const uint32_t rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
+  return kAbInstances && a.R <= 4 && a.K >= kTriDbMinK && !(a.in_misalign | a.out_misalign) &&
+         (a.verify_mask & rows) == 0;
+}
 bool can_dma(const ApplyArgs& a) {
   return kAbInstances && a.R <= 8 && a.K >= 2 && !(a.in_misalign | a.out_misalign) &&
          dev::lds_bytes_dma(a.K, a.R, kDmaDepth) <= (64u << 10);
@@ -676,6 +685,10 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
       if (tps > 1024 || (every_instance && tps >= 64)) add(tri_in(TileOrder::kSeg16));
       if (tps > 1024 || every_instance) add(tri_in(TileOrder::kXcd8));
     }
+    if (every_instance && can_tridb_g(a)) {  // G4 / G8 double-buffered triples: A/B build only
+      add(static_cast<TileOrder>(kOrderTriDbG));
+      add(static_cast<TileOrder>(kOrderTriDbG + 1));
+    }
     if (every_instance && can_dma(a)) {  // the LDS-DMA ring: A/B build only
       for (TileOrder o : {TileOrder::kConsecutive, TileOrder::kGroup2, TileOrder::kSeg8, TileOrder::kXcd32})
         add(static_cast<TileOrder>(kOrderDma + static_cast<int>(o)));
@@ -699,6 +712,12 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
+  // (A/B) the double-buffered triples in G4 / G8: the nibble instances' G8 order underneath
+  int tdg = -1;
+  if (order >= kOrderTriDbG) {
+    tdg = can_tridb_g(a) ? order - kOrderTriDbG : -1;
+    order = tdg >= 0 ? static_cast<int>(TileOrder::kGroup8) : -1;
+  }
   const bool dma = order >= kOrderDma && can_dma(a);
   if (order >= kOrderDma) order = dma ? order - kOrderDma : -1;
   // realigning kernel with triple loads: kOrderRealignTri + its order -> kOrderRealign + it
@@ -765,6 +784,9 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
             fn = kLdsDma[dma_index(ord)][a.R - 1];
             lds = dev::lds_bytes_dma(a.K, a.R, kDmaDepth);
           }
+          if (tdg >= 0) fn = kLdsTriDbG[tdg][a.R - 1];
+#else
+          (void)tdg;
 #endif
         } else if ((order >= 0 ? static_cast<TileOrder>(order) : wide_rule(a)) == TileOrder::kSeg8) {
           fn = kLdsWideQ8[a.R - 9];
@@ -917,7 +939,9 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
   a.tail_in_vec = a.nvec * 16 < a.S ? tail_code(a.nvec, LdsPolicy::TILE_VECS, LdsPolicy::BS) : 0u;
-  if (order >= kOrderRealign64) order = order - kOrderRealign64 + kOrderRealign;
+  if (order >= kOrderTriDbG) order = static_cast<int>(TileOrder::kGroup8);  // (A/B forms:
+  else if (order >= kOrderDma) order -= kOrderDma;                          //  their tile order)
+  else if (order >= kOrderRealign64) order = order - kOrderRealign64 + kOrderRealign;
   else if (order >= kOrderRealignTri) order = order - kOrderRealignTri + kOrderRealign;
   else if (order >= kOrderTri) order -= kOrderTri;
   if (order >= kOrderWix) order -= kOrderWix;  // bounded by the nibble kernel's traffic

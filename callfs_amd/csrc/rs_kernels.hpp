@@ -134,6 +134,9 @@ constexpr int kOrderRealign64 = 160;
 // (kOrderDma + consecutive / G2 / Q8 / X32: aligned R <= 8 launches with their input vectors
 // staged through an LDS-DMA ring, rs_apply.hpp Policy::DMA; A/B build)
 constexpr int kOrderDma = 192;
+// (kOrderTriDbG + 0 / 1: R <= 4, K >= 6 double-buffered triples with the tiles of 4 / 8 stripes
+// interleaved (G4 / G8); A/B build)
+constexpr int kOrderTriDbG = 224;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the

@@ -1227,7 +1227,7 @@ ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign
                    "realign-x8", "realign-x32", "wix", "wix-g8", "wix-g2", "wix-q8", "wix-q16",
                    "wix-x8", "wix-x32", "tri", "tri-g2", "tri-x32", "tri-q8", "tri-q16",
                    "tri-x8", "realign-tri", "realign-tri-x8", "realign-tri-x32",
-                   "dma", "dma-g2", "dma-q8", "dma-x32"]
+                   "dma", "dma-g2", "dma-q8", "dma-x32", "tridb-g4", "tridb-g8"]
 
 
 @pytest.mark.parametrize("k,m,S,batch,off,erase", [
@@ -1298,7 +1298,7 @@ def test_plan_every_offered_order_bit_exact(native_lib, k, m, S, batch, off, era
     # product refuses them (run with CALLFS_RS_LIB=callfs_amd/libcallfs_rs_ab.so, the A/B
     # build offers and checks them here)
     if "libcallfs_rs_ab" not in N.LIB_PATH:
-        assert not any(t.startswith(("wix", "dma")) for t in taken), taken
+        assert not any(t.startswith(("wix", "dma", "tridb-")) for t in taken), taken
     with pytest.raises(N.NativeError):
         plan.set_orders(["none"] * (plan_groups := int(N.lib.rs_plan_groups(plan.handle))) + ["none"])
     plan.set_orders(["none"] * plan_groups)
