@@ -12,6 +12,13 @@ over that batch:
 value = user bytes through both ops (2 * stripes * k * S per GPU per step) summed over
 all ranks / the max-over-ranks wall time of the timed steps, in GiB/s.
 
+Layout (since round 4; rounds 1-3 kept each stripe's n shards in one block, `--layout
+pitch`): the data shards in one HBM region and the parity in another (`planar`), erased
+shards rebuilt into fresh buffers. At the metric's 1 MiB shards these are the bytes upstream
+Split of a 10 MiB io.ReadAll body lays out (data at a 1 MiB pitch in the body, parity in
+AllocAligned buffers) and the buffers upstream Reconstruct allocates; `layout_ab.pitch` in
+the line times the same kernels in the old layout in the same process.
+
 Multi-GPU: one process per GPU (torch.distributed.run); stripes are independent, so
 each rank encodes/decodes its own batch with no data-path collective ("weak"
 scaling). The only cross-rank traffic is the gloo barrier and the max-reduce of the
