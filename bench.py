@@ -14,9 +14,10 @@ all ranks / the max-over-ranks wall time of the timed steps, in GiB/s.
 
 Layout (since round 4; rounds 1-3 kept each stripe's n shards in one block, `--layout
 pitch`): the data shards in one HBM region and the parity in another (`planar`), erased
-shards rebuilt into fresh buffers. At the metric's 1 MiB shards these are the bytes upstream
-Split of a 10 MiB io.ReadAll body lays out (data at a 1 MiB pitch in the body, parity in
-AllocAligned buffers) and the buffers upstream Reconstruct allocates; `layout_ab.pitch` in
+shards rebuilt into fresh buffers. At the metric's 1 MiB shards this is how upstream Split
+lays out a 10 MiB io.ReadAll body whose capacity ends at its length (data at a 1 MiB pitch
+in the body, parity in AllocAligned buffers), and the buffers upstream Reconstruct
+allocates; `layout_ab.pitch` in
 the line times the same kernels in the old layout in the same process.
 
 Multi-GPU: one process per GPU (torch.distributed.run); stripes are independent, so
