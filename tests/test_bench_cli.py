@@ -49,7 +49,8 @@ def test_committed_traffic_matches_the_default_bench_config():
 @pytest.mark.parametrize("extra", [[], ["--decode-into", "inplace"], ["--layout", "pitch"],
                                    ["--split-layout", "readall", "--shard-bytes", "100003"],
                                    ["--split-layout", "--shard-bytes", "100003"],
-                                   ["--pitch", str((1 << 20) + 4096)]])
+                                   ["--pitch", str((1 << 20) + 4096)],
+                                   ["--object-bytes", str(16 << 20)]])
 def test_bench_layouts_run_and_check(extra):
     """bench.py end to end on a small batch in every layout it offers: the device round
     trip, the timed steps, the rebuilt-shard check, the ceilings and (planar) the
