@@ -113,12 +113,13 @@ struct Policy {
   static_assert(DMA_ == 0 || (REALIGN_ == 0 && WIX_ == 0 && RING_ == 0 && !NOMATH_ && !SDWA_ &&
                               VPF_ == 0 && PROBE_ == 0 && BS_ == 512 && U_ == 1),
                 "DMA: aligned ring-of-three kernel shape only");
-  // LDS kernel, R <= 4, plain ring-of-three loop: input shards in triples, each byte
-  // position of a triple resolved by four 6-bit lookups into 64-entry tables of 4-byte
-  // entries (built in LDS from the nibble tables) instead of six nibble lookups; Verify
-  // rows load their compared vectors after the input loop
-  // (WIX 2, A/B probe: the same triple loop with the nibble lookups, any R <= 8)
-  // (WIX 2 with REALIGN: the realigning kernel's aligned loads issued in triples)
+  // 1 (A/B build): R <= 4, input shards in triples, each byte position of a triple
+  // resolved by four 6-bit lookups into 64-entry tables of 4-byte entries (built in LDS
+  // from the nibble tables) instead of six nibble lookups;
+  // 2: the same triple loads with the nibble lookups, any R <= 8 (production);
+  // 2 with REALIGN: the realigning kernel's aligned loads issued in triples;
+  // 3: triples double-buffered in two register sets (production for R <= 4, K >= 6);
+  // 4 (kbench probe): as 1 with zeros past K; 5 (kbench probe): as 3 with pairs
   static constexpr int WIX = WIX_;
   // (WIX 2 with VPF: the aligned triple loop with early compare loads)
   static_assert(!WIX_ || ((REALIGN_ == 0 || WIX_ == 2 || (WIX_ == 3 && REALIGN_ == 2)) && (VPF_ == 0 || ((WIX_ == 2 || WIX_ == 3) && REALIGN_ == 0)) &&
