@@ -1685,3 +1685,40 @@ def test_plan_double_buffered_triples_vs_oracle(native_lib, k, m):
         for b in range(batch):
             for j in range(m):
                 assert np.array_equal(got[b, k + j, :S], want[b][j]), (order, b, j)
+
+
+@pytest.mark.parametrize("k,m,S,batch", [
+    (8, 4, 2 << 20, 3),            # K 7..9, 1-2 MiB: double-buffered triples in G2
+    (8, 4, (8 << 20) - 16 * 3 - 1, 2),  # K 7..9 above 2 MiB: the ring, consecutive (ragged tail)
+    (10, 4, (2 << 20) + 7, 3),     # K >= 10 above 1 MiB: the ring
+    (8, 8, 2 << 20, 3),            # R 5..8, 1-2 MiB, K < 10: triples, consecutive
+    (10, 8, 1_677_722, 3),         # R 5..8, K 10..12 to 2 MiB: triples in Q8
+    (10, 8, 6_710_887 // 2, 2),    # R 5..8 to 8 MiB: triples in X32
+    (8, 8, 131_072, 5),            # R 5..8 up to 256 KiB: triples in G2
+    (20, 4, 52_429, 9),            # R <= 4, K > 16, small: double-buffered triples in G2
+    (20, 4, 838_861, 3),           # K > 16, 256 KiB - 1 MiB: the ring, consecutive
+    (32, 8, 2 << 20, 2),           # K > 16 with 8 rows above 1 MiB: the ring, consecutive
+])
+def test_planar_rule_forms_vs_oracle(native_lib, k, m, S, batch):
+    """The round-5 rule (tile_order.hpp, fitted on the planar layout) picks a different form
+    or order on these shapes than round 4's: the rule's own launch, on a planar batch,
+    against the oracle on every byte of every stripe, and the m-erasure decode of the data
+    shards in front restores them."""
+    import torch
+    from callfs_amd.device import Plan, StripeBatch
+    sb = StripeBatch(k, m, S, batch, torch.device("cuda:0"), layout="planar")
+    sb.fill_random(S + 7 * k + m)
+    Plan.for_batch(sb).launch()
+    torch.cuda.synchronize()
+    h = sb.gather().cpu().numpy()
+    for b in range(batch):
+        want = cref.encode([h[b, i] for i in range(k)], k, m)
+        for j in range(m):
+            assert np.array_equal(h[b, k + j], want[j]), (b, j)
+    erase = list(range(min(m, k)))
+    for i in erase:
+        sb.zero_shard(i)
+    dec = Plan.for_batch(sb, present=[i not in erase for i in range(k + m)])
+    dec.launch()
+    assert not dec.corrupt()
+    assert np.array_equal(sb.gather().cpu().numpy(), h)
