@@ -118,6 +118,9 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
                                 uint64_t stripe_stride, bool verify = false,
                                 bool read_only = false, int rows = 8) {
   if (read_only && tps > 32) return TileOrder::kXcd32;
+  // (round 5, planar: read-only launches of 5-8 rows up to 256 KiB run the ring fastest in
+  // consecutive order, RS(10,8) 104,858 B 76.5; profiles/r05/decode_rule/)
+  if (read_only && rows >= 5) return TileOrder::kConsecutive;
   // stripes exactly 2 MiB apart: interleaving stripes costs 2-12 points (RS(8,8) 128 KiB
   // 72.4 -> 60.6 with G8, RS(4,4) 256 KiB 77.9 -> 65.8, RS(6,2) 256 KiB 81.5 -> 78.4);
   // strides of 1, 4, 8 or 16 MiB interleave fine (profiles/r01/tile_order/segments/
@@ -191,11 +194,17 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
   const bool pow2_16_32 = addr_tz >= 24 && S >= (16ull << 20) && S <= (32ull << 20);
   // R <= 4 with K >= 6 runs the double-buffered form (rs_kernels.hip kTriDbMinK)
   const bool db = R <= 4 && K >= 6;
+  const int cons = static_cast<int>(TileOrder::kConsecutive);
   if (verify && !read_only) {  // written + Verify rows: only the R <= 4 early-compare forms
     if (R > 4) return -1;
     if (K <= 4) return x32;
     if (db) {  // round 4 (profiles/r04/tri_verify_ab2): G2 up to 1 MiB, X32 above
-      if (K > 16 || tps <= 32) return tps <= 32 && K <= 6 ? x32 : -1;
+      // round 5, planar (tools/decode_rule_sweep.sh, profiles/r05/decode_rule/): up to 256 KiB
+      // the early-compare triples in G2 for K >= 7, where the ring ran (RS(10,4) 104,858 B
+      // erase {1} 71.0 -> 75.7, {10} 72.0 -> 76.9; RS(12,4) 87,382 B {1} 69.3 -> 75.2; RS(8,4)
+      // 128 KiB {1} 74.6 -> 77.6; RS(16,4) 64 KiB {1} 70.5 -> 77.3)
+      if (tps <= 32) return K <= 6 ? x32 : g2;
+      if (K > 16) return -1;
       return tps <= 128 ? g2 : x32;
     }
     if (tps <= 32) return x32;
@@ -221,6 +230,19 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     if (tps <= 256) return g2;
     if (tps <= 1024) return -1;
     return pow2_16_32 ? q16 : -1;
+  }
+  // Read-only launches (every row compared: the download with nothing lost), round 5, planar
+  // (tools/decode_rule_sweep.sh, profiles/r05/decode_rule/): R 5..8 keep the ring, which
+  // runs 5-7 points ahead of the rotating triples there (RS(10,8) 104,858 B tri-X32 71.6 ->
+  // ring 76.5, 1.68 MB 71.1 -> 78.3, 6.7 MB 72.1 -> 78.1); R <= 4 take the triples up to 256
+  // KiB in consecutive order (RS(16,4) 64 KiB ring 78.3 -> 83.7, RS(12,4) 87,382 B 78.2 ->
+  // 81.5, RS(10,4) 104,858 B 79.5 -> 82.3, RS(8,4) 128 KiB 83.1 -> 84.9) and with K > 12 above
+  // it too, in Q8 to 1 MiB and X32 above (RS(16,4) 1 MiB ring 78.5 -> tri-Q8 83.3, 4 MiB 77.9
+  // -> tri-X32 81.0)
+  if (read_only) {
+    if (R > 4) return -1;
+    if (tps <= 32) return cons;
+    if (K > 12) return tps <= 128 ? q8 : x32;
   }
   // R 5..8 on shards up to 256 KiB: the rotating triples in X32 for any K (round 4,
   // planar 1 MiB objects, tools/small_r8_probe.sh, profiles/r04/smallr8/ab.jsonl: RS(32,8)
