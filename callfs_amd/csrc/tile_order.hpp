@@ -205,7 +205,9 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
       // 128 KiB {1} 74.6 -> 77.6; RS(16,4) 64 KiB {1} 70.5 -> 77.3)
       if (tps <= 32) return K <= 6 ? x32 : g2;
       if (K > 16) return -1;
-      return tps <= 128 ? g2 : x32;
+      // (round 5: G2 to 2 MiB, RS(10,4) 1.68 MB {1} X32 74.7 -> G2 75.5, RS(12,4) 1.4 MB
+      // {12} 73.4 -> 74.5)
+      return tps <= 256 ? g2 : x32;
     }
     if (tps <= 32) return x32;
     return tps <= 128 ? static_cast<int>(tri_order(nibble)) : -1;
@@ -243,6 +245,9 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     if (R > 4) return -1;
     if (tps <= 32) return cons;
     if (K > 12) return tps <= 128 ? q8 : x32;
+    // K 10..12 above 2 MiB in Q8 (RS(10,4) 6.7 MB X32 82.9 / 81.9 -> 83.9 / 83.4, RS(12,4)
+    // 5.6 MB 82.3 / 81.1 -> 82.8 / 82.1)
+    if (K >= 10 && tps > 256) return q8;
   }
   // R 5..8 on shards up to 256 KiB: the rotating triples in X32 for any K (round 4,
   // planar 1 MiB objects, tools/small_r8_probe.sh, profiles/r04/smallr8/ab.jsonl: RS(32,8)
