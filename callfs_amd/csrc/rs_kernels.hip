@@ -539,6 +539,10 @@ int tri_unaligned_order(const ApplyArgs& a, uint64_t tps) {
   if (a.R > 8 || a.K < 4 || !a.in_misalign || a.out_misalign || tile_order_override() >= 0)
     return -1;
   if (a.K > 12 && tps > 32) return -1;
+  // round 5 (tools/readall_rule_sweep.sh, profiles/r05/readall_rule/): Q8 from 1 to 2 MiB,
+  // X32 -> Q8: RS(10,4) 1.68 MB 74.9 -> 76.6, RS(12,4) 1.4 MB 75.1 -> 76.3, RS(8,8) 2 MiB
+  // 75.0 -> 76.3, RS(10,8) 1.68 MB 70.4 -> 71.7
+  if (tps > 128 && tps <= 256) return static_cast<int>(TileOrder::kSeg8);
   return static_cast<int>(tps <= 256 ? TileOrder::kXcd32 : TileOrder::kXcd8);
 }
 

@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tune", type=int, default=0)
+    ap.add_argument("--fresh", type=int, default=0,
+                    help="1: decodes rebuild the erased shards into fresh buffers instead of in place")
     ap.add_argument("--only", default="",
                     help="comma-separated variants to time (prod,tuned,nolookup,read,write); "
                          "default all (rocprofv3 --pmc passes time only prod)")
@@ -102,6 +104,18 @@ def main():
         else:
             er = {int(x) for x in erase.split("+")}
             present = [i not in er for i in range(n)]
+        fresh_buf = None
+        if present is not None and a.fresh and not all(present):
+            # the erased shards rebuilt into a region of their own (64-B pitch, 256-B aligned),
+            # as upstream Reconstruct allocates missing shards (bench.py --decode-into fresh)
+            from callfs_amd.device import _aligned_empty
+            miss = [i for i in range(n) if not present[i]]
+            fp = -(-S // 64) * 64
+            fresh_buf = _aligned_empty((B, len(miss), fp), 256, dev)
+            ptrs = list(ptrs)
+            for b in range(B):
+                for j, i in enumerate(miss):
+                    ptrs[b * n + i] = fresh_buf[b, j].data_ptr()
         plan = enc if present is None else Plan(k, m, S, B, ptrs, present=present)
         variants = {"prod": lambda: plan.launch(stream)}
         orders = None
@@ -137,7 +151,7 @@ def main():
                "ms": {v: round(x, 4) for v, x in best.items()}, "tuned_orders": orders,
                "verify_after": bool(bad)}
         print(json.dumps(out), flush=True)
-        del plan, enc, holder
+        del plan, enc, holder, fresh_buf
         torch.cuda.empty_cache()
 
 

@@ -1,7 +1,8 @@
 # The profile sweep's 33 cells in the layout CallFS produces (upstream Split of an io.ReadAll
 # body: data shards at pitch S in the body, parity in 64-B AllocAligned buffers), encode and a
-# two-data-shard decode written back in place, rule against rs_plan_tune (tools/ceiling_sweep.py).
-# Usage: bash tools/readall_rule_sweep.sh <tag>
+# two-data-shard decode (in place; FRESH=1: into fresh buffers, as upstream Reconstruct
+# allocates them), rule against rs_plan_tune (tools/ceiling_sweep.py).
+# Usage: [FRESH=1] bash tools/readall_rule_sweep.sh <tag>
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; TAG="${1:-readall_rule}"; O="$R/gpurun_out/$TAG"; mkdir -p "$O"; cd "$R"
 A=()
@@ -12,6 +13,6 @@ for km in "4 2" "3 2" "6 3" "8 4" "10 4" "12 4" "16 4" "8 8" "10 8" "20 4" "32 8
     A+=(--shape "$k,$m,$S,$B,-,readall" --shape "$k,$m,$S,$B,0+1,readall")
   done
 done
-timeout -k 10 1300 python3 -u tools/ceiling_sweep.py --tune 1 --rounds 2 --only prod,tuned "${A[@]}" \
+timeout -k 10 1300 python3 -u tools/ceiling_sweep.py --tune 1 --rounds 2 --only prod,tuned --fresh "${FRESH:-0}" "${A[@]}" \
   > "$O/sweep.jsonl" 2>&1 || exit $?
 echo "readall sweep ok"
