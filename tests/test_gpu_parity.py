@@ -1531,7 +1531,7 @@ def test_plan_ceiling_split_layout_stays_inside_written_shards(native_lib, k, m,
     (10, 4, 1 << 16, 3),                # 16 | S: every shard aligned
 ])
 @pytest.mark.parametrize("how", ["rule", "tune", "realign-x32", "realign", "realign-tri-x32",
-                                 "tri-x32", "tri-g2", "tri-x8"])
+                                 "tri-x32", "tri-g2", "tri-x8", "tri-q8"])
 def test_readall_layout_round_trip(native_lib, k, m, S, batch, how):
     """Upstream Split of an io.ReadAll body (StripeBatch layout "readall": data shards at
     pitch S inside the body, parity in 64-B AllocAligned buffers at a 64-B pitch): encode
@@ -1575,6 +1575,56 @@ def test_readall_layout_round_trip(native_lib, k, m, S, batch, how):
         dec.launch()
         assert not dec.corrupt(), erase
         assert np.array_equal(sb.gather().cpu().numpy(), host), erase
+
+
+@pytest.mark.parametrize("k,m,S,batch", [
+    (10, 4, 100_003, 3),
+    (10, 4, 1_677_722 + 1, 2),          # 205 tiles per shard: the readall rule's Q8 band
+    (6, 3, 16 * 496 + 16 * 62 + 5, 4),
+    (12, 4, 5_592_406 // 64, 2),
+])
+@pytest.mark.parametrize("how", ["rule", "tune", "tri-x32", "tri-q8", "tri-g2", "realign-x32"])
+def test_readall_decode_into_fresh_buffers(native_lib, k, m, S, batch, how):
+    """The decode CallFS runs on an io.ReadAll body (bench.py --layout readall --decode-into
+    fresh): survivors at odd offsets in the body, the erased shards rebuilt into buffers of
+    their own (64-B pitch, 256-B aligned), as upstream Reconstruct allocates missing shards.
+    Misaligned inputs with aligned outputs take the unaligned triples (tri_unaligned_order);
+    every rebuilt shard equals the encoded original, for each pinned form the launch offers."""
+    import torch
+    from callfs_amd import _native as N
+    from callfs_amd.device import Plan, StripeBatch, _aligned_empty
+    n = k + m
+    sb = StripeBatch(k, m, S, batch, torch.device("cuda:0"), layout="readall")
+    sb.fill_random(S + 7 * k)
+    Plan.for_batch(sb).launch()
+    torch.cuda.synchronize()
+    host = sb.gather().cpu().numpy()
+    for b in range(batch):
+        want = cref.encode([host[b, i] for i in range(k)], k, m)
+        assert all(np.array_equal(host[b, k + j], want[j]) for j in range(m)), b
+    fp = -(-S // 64) * 64
+    for erase in (list(range(0, k, max(1, k // m)))[:m], [1, k], [0, 3]):
+        fresh = _aligned_empty((batch, len(erase), fp), 256, torch.device("cuda:0"))
+        fresh.fill_(0xA5)
+        ptrs = list(sb.pointers())
+        for b in range(batch):
+            for j, i in enumerate(erase):
+                ptrs[b * n + i] = fresh[b, j].data_ptr()
+        dec = Plan(k, m, S, batch, ptrs, present=[i not in erase for i in range(n)])
+        if how == "tune":
+            dec.tune(reps=1)
+        elif how != "rule":
+            try:
+                dec.set_orders([how] * int(N.lib.rs_plan_groups(dec.handle)))
+            except N.NativeError as e:  # not offered for this launch: the rule's kernel
+                assert e.code == N.RS_E_ARG
+        dec.launch()
+        assert not dec.corrupt(), erase
+        got = fresh.cpu().numpy()
+        for b in range(batch):
+            for j, i in enumerate(erase):
+                assert np.array_equal(got[b, j, :S], host[b, i]), (erase, b, i)
+        del dec, fresh
 
 
 @pytest.mark.parametrize("k,m,L", [(10, 4, 10 * 1000 + 7), (4, 2, 4 * 37 + 1), (16, 4, 4096)])

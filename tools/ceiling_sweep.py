@@ -6,14 +6,15 @@ alone + write streams alone (rs_plan_launch_ceiling), interleaved over rounds in
 process; every variant is warmed >= 30 ms before it is timed. Prints one JSON line per
 shape with % of 8 TB/s (algorithmic bytes / mean launch time) for each.
 
-shape spec: k,m,S,stripes[,erase[,layout]]   erase: '-' = encode, 'none' = all present,
+shape spec: k,m,S,stripes[,erase[,layout[,order]]]   erase: '-' = encode, 'none' = all present,
             or '+'-joined indices (5, 0+3+7+12); layout: 'pitch' (StripeBatch, 256-B
             pitch, default), 'split' (upstream Split layout: object b's shard i at
             base + (b*n + i)*S from an odd base, every shard at its own byte offset when
             S is odd), 'contig' (the same from an aligned base) or 'readall' (Split of an
             io.ReadAll body: data shards at pitch S in page-aligned bodies, parity in
             64-B AllocAligned buffers; device.StripeBatch); 'planar:P' / 'pitch:P' set
-            the shard pitch to P bytes
+            the shard pitch to P bytes; order: the plan's launches pinned to that tile order
+            / kernel form (device.ORDER_NAMES, rs_plan_set_orders) instead of the rule's
 usage: python tools/ceiling_sweep.py --shape 10,4,1048576,256,5 --shape ... [--tune 1]
 """
 import argparse
@@ -86,6 +87,7 @@ def main():
         k, m, S, B = (int(x) for x in f[:4])
         erase = f[4] if len(f) > 4 else "-"
         layout = f[5] if len(f) > 5 else "pitch"
+        pin = f[6] if len(f) > 6 else ""
         n = k + m
         if erase not in ("-", "none") and (len({int(x) for x in erase.split("+")}) > m or
                                            max(int(x) for x in erase.split("+")) >= n):
@@ -117,6 +119,9 @@ def main():
                 for j, i in enumerate(miss):
                     ptrs[b * n + i] = fresh_buf[b, j].data_ptr()
         plan = enc if present is None else Plan(k, m, S, B, ptrs, present=present)
+        if pin:
+            from callfs_amd import _native as N
+            plan.set_orders([pin] * int(N.lib.rs_plan_groups(plan.handle)))
         variants = {"prod": lambda: plan.launch(stream)}
         orders = None
         if a.tune:
@@ -147,7 +152,7 @@ def main():
             if "prod" in pct:
                 pct["prod/read+write"] = round(pct["prod"] / rw, 4)
         out = {"shape": spec, "k": k, "m": m, "S": S, "stripes": B, "erase": erase,
-               "layout": layout, "bytes": nb, "pct_of_8TBs": pct,
+               "layout": layout, "order": pin or "rule", "bytes": nb, "pct_of_8TBs": pct,
                "ms": {v: round(x, 4) for v, x in best.items()}, "tuned_orders": orders,
                "verify_after": bool(bad)}
         print(json.dumps(out), flush=True)
