@@ -7,7 +7,8 @@
 // Prints GB/s per variant, best of `reps` launches, after a warm-up.
 //
 // build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/write_pattern.hip -o tools/write_pattern
-// run:   tools/write_pattern [reps]
+// run:   tools/write_pattern [reps] [pitch]   (pitch: rows of 1 MiB shards at 1, 2, 6.4
+//         and 8 MiB pitch, then 6.4 MiB shards; does the written span's contiguity matter?)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -94,25 +95,40 @@ int main(int argc, char** argv) {
     const char* name;
     uint64_t S;
     uint32_t R, order, g, read, rowwave, bs;
+    uint64_t pitch;  // 0: S
   };
   std::vector<V> vs;
   const uint64_t shapes[] = {1ull << 20, 2ull << 20, 6710912, 8ull << 20, 64ull << 20};
-  for (uint32_t bs : {128u, 256u, 512u, 1024u})
-    for (uint64_t S : shapes)
-      for (uint32_t R : {1u, 4u, 8u}) {
-        vs.push_back({"consecutive", S, R, 0, 0, 0, 0, bs});
-        vs.push_back({"G8", S, R, 1, 8, 0, 0, bs});
-        vs.push_back({"Q8", S, R, 2, 8, 0, 0, bs});
-      }
-  std::printf("variant,shard_bytes,rows,block,mode,GBps\n");
+  if (argc > 2) {
+    const uint64_t pitches[] = {1ull << 20, (2ull << 20) + 256, 6710912, 8ull << 20};
+    for (int rep = 0; rep < 2; ++rep)
+      for (uint64_t P : pitches)
+        for (uint32_t R : {1u, 4u}) {
+          vs.push_back({"consecutive", 1ull << 20, R, 0, 0, 0, 0, 512, P});
+          vs.push_back({"G8", 1ull << 20, R, 1, 8, 0, 0, 512, P});
+          if (P == 6710912) {
+            vs.push_back({"consecutive", P, R, 0, 0, 0, 0, 512, P});
+            vs.push_back({"G8", P, R, 1, 8, 0, 0, 512, P});
+          }
+        }
+  } else {
+    for (uint32_t bs : {128u, 256u, 512u, 1024u})
+      for (uint64_t S : shapes)
+        for (uint32_t R : {1u, 4u, 8u}) {
+          vs.push_back({"consecutive", S, R, 0, 0, 0, 0, bs, 0});
+          vs.push_back({"G8", S, R, 1, 8, 0, 0, bs, 0});
+          vs.push_back({"Q8", S, R, 2, 8, 0, 0, bs, 0});
+        }
+  }
+  std::printf("variant,shard_bytes,pitch,rows,block,mode,GBps\n");
   for (const V& v : vs) {
     Args a{};
     a.base = buf;
-    a.pitch = v.S;
+    a.pitch = v.pitch ? v.pitch : v.S;
     a.R = v.R;
     const uint64_t tb = v.bs * 16ull;
     a.tps = static_cast<uint32_t>(v.S / tb);
-    a.batch = static_cast<uint32_t>(total / (v.S * v.R));
+    a.batch = static_cast<uint32_t>(total / (a.pitch * v.R));
     a.order = v.order;
     a.g = v.g;
     a.read = v.read;
@@ -136,8 +152,9 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       best = ms < best ? ms : best;
     }
-    std::printf("%s,%llu,%u,%u,%s,%.0f\n", v.name, static_cast<unsigned long long>(v.S), v.R,
-                v.bs, v.read ? "read" : "write", bytes / (best * 1e-3) / 1e9);
+    std::printf("%s,%llu,%llu,%u,%u,%s,%.0f\n", v.name, static_cast<unsigned long long>(v.S),
+                static_cast<unsigned long long>(a.pitch), v.R, v.bs, v.read ? "read" : "write",
+                bytes / (best * 1e-3) / 1e9);
     std::fflush(stdout);
   }
   CK(hipFree(buf));
