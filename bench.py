@@ -17,8 +17,9 @@ pitch`): the data shards in one HBM region and the parity in another (`planar`),
 shards rebuilt into fresh buffers. At the metric's 1 MiB shards this is how upstream Split
 lays out a 10 MiB io.ReadAll body whose capacity ends at its length (data at a 1 MiB pitch
 in the body, parity in AllocAligned buffers), and the buffers upstream Reconstruct
-allocates; `layout_ab.pitch` in
-the line times the same kernels in the old layout in the same process.
+allocates; `layout_ab` in the line times the same kernels in the same process in the old
+layout (`pitch`) and in upstream Split of an io.ReadAll body per object (`readall`, decode
+into fresh buffers).
 
 Multi-GPU: one process per GPU (torch.distributed.run); stripes are independent, so
 each rank encodes/decodes its own batch with no data-path collective ("weak"
@@ -87,7 +88,8 @@ def parse_args(argv=None):
                         "missing shards) or into their slots of the batch ('inplace')")
     p.add_argument("--layout-ab", type=int, default=1,
                    help="1: with --layout planar, also time the same workload's kernels in the "
-                        "'pitch' layout in this process (tuned as well): line['layout_ab']")
+                        "'pitch' and 'readall' layouts in this process (tuned as well): "
+                        "line['layout_ab']")
     p.add_argument("--split-layout", nargs="?", const="split", default=None,
                    choices=("split", "readall"),
                    help="upstream Split layout (codec.go:31) instead of the 256-B shard "
@@ -289,30 +291,49 @@ def plan_ceilings(enc, dec, stream):
 
 
 def layout_ab(k, m, S, B, dev, present, stream, tune, pitch=None):
-    """The same encode and decode in the 'pitch' layout (256-B shard pitch, each stripe's n
-    shards in one block, the bench layout of rounds 1-3), timed in this process after the
-    bench's own plans: a second batch, its plans tuned as the bench's are, mean kernel time
-    of 20 event-timed launches after >= 30 ms of warmup each (_launch_ms)."""
-    from callfs_amd.device import Plan, StripeBatch
-    sb = StripeBatch(k, m, S, B, dev, layout="pitch", pitch=pitch)
-    sb.fill_random(0x5EED)
-    enc, dec = Plan.for_batch(sb), Plan.for_batch(sb, present=present)
-    enc.launch(stream)
-    orders = ({"encode": enc.tune(stream=stream), "decode": dec.tune(stream=stream)}
-              if tune else None)
-    out = {"pitch": {"tile_order": orders}}
-    for name, plan in (("encode", enc), ("decode", dec)):
-        ms = _launch_ms(lambda evs: plan.launch(stream, events=evs), stream)
-        out["pitch"][name + "_frac"] = round(plan.bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-    if dec.corrupt(stream):
-        raise SystemExit("pitch-layout decode flagged corruption")
-    enc.close()
-    dec.close()
-    del sb
-    torch.cuda.empty_cache()
+    """The same encode and decode in two more layouts, timed in this process after the
+    bench's own plans: 'pitch' (256-B shard pitch, each stripe's n shards in one block, the
+    bench layout of rounds 1-3; decode in place) and 'readall' (upstream Split of an
+    io.ReadAll body per object: data at pitch S in the body, parity in AllocAligned buffers;
+    decode into fresh buffers, as Reconstruct allocates the missing shards). Each a second
+    batch, its plans tuned as the bench's are, mean kernel time of 20 event-timed launches
+    after >= 30 ms of warmup each (_launch_ms)."""
+    from callfs_amd.device import Plan, StripeBatch, _aligned_empty
+    out = {}
+    erase = [i for i in range(k + m) if not present[i]]
+    for layout in ("pitch", "readall"):
+        sb = StripeBatch(k, m, S, B, dev, layout=layout,
+                         pitch=pitch if layout == "pitch" else None)
+        sb.fill_random(0x5EED)
+        enc = Plan.for_batch(sb)
+        rebuilt = None
+        if layout == "readall":
+            rebuilt = _aligned_empty((B, len(erase), sb.par_pitch), 256, dev)
+            ptrs = sb.pointers()
+            for b in range(B):
+                for j, i in enumerate(erase):
+                    ptrs[b * (k + m) + i] = rebuilt[b, j].data_ptr()
+            dec = Plan(k, m, S, B, ptrs, present=present)
+        else:
+            dec = Plan.for_batch(sb, present=present)
+        enc.launch(stream)
+        orders = ({"encode": enc.tune(stream=stream), "decode": dec.tune(stream=stream)}
+                  if tune else None)
+        r = out[layout] = {"tile_order": orders}
+        for name, plan in (("encode", enc), ("decode", dec)):
+            ms = _launch_ms(lambda evs: plan.launch(stream, events=evs), stream)
+            r[name + "_frac"] = round(plan.bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if dec.corrupt(stream):
+            raise SystemExit(f"{layout}-layout decode flagged corruption")
+        if rebuilt is not None and not torch.equal(rebuilt[:, :, :S], sb.gather()[:, erase]):
+            raise SystemExit("readall-layout decode rebuilt wrong bytes")
+        enc.close()
+        dec.close()
+        del sb, rebuilt
+        torch.cuda.empty_cache()
     out["note"] = ("kernel-time fractions of 8 TB/s, same workload, same process: the bench "
                    "layout ('planar') against each stripe's data and parity in one block "
-                   "('pitch'); DESIGN.md §4")
+                   "('pitch') and upstream Split of an io.ReadAll body ('readall'); DESIGN.md §4")
     return out
 
 

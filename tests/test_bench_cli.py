@@ -54,7 +54,7 @@ def test_committed_traffic_matches_the_default_bench_config():
 def test_bench_layouts_run_and_check(extra):
     """bench.py end to end on a small batch in every layout it offers: the device round
     trip, the timed steps, the rebuilt-shard check, the ceilings and (planar) the
-    in-process pitch-layout A/B all pass, and the line parses."""
+    in-process pitch / readall layout A/B all pass, and the line parses."""
     import json
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stripes", "8",
@@ -66,4 +66,8 @@ def test_bench_layouts_run_and_check(extra):
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
     assert line["cpu_baseline"]["parity_check"].startswith("GPU parity")
     if not extra:
-        assert "layout_ab" in line and line["config"]["layout"] == "planar"
+        assert line["config"]["layout"] == "planar"
+        ab = line["layout_ab"]
+        assert "error" not in ab, ab
+        for lay in ("pitch", "readall", "planar"):
+            assert 0 < ab[lay]["encode_frac"] < 1 and 0 < ab[lay]["decode_frac"] < 1, lay
