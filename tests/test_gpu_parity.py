@@ -914,6 +914,69 @@ def test_random_plans_vs_oracle(native_lib, k, m, S, batch, off, erase):
     assert torch.equal(buf, ref)
 
 
+def _random_layout_cases(n=36, seed=0x5A17):
+    """Seeded (layout, k, m, S, batch, erasures, fresh) draws over the layouts the round-5
+    rules were fitted on: planar (256-B pitch), readall (upstream Split of an io.ReadAll
+    body: odd S puts every data shard at its own offset) and split (pitch S, odd base), with
+    shard sizes spanning each rule band (<= 256 KiB, to 1 MiB, the 1-2 MiB Q8 band, above)."""
+    rng = np.random.default_rng(seed)
+    sizes = [4_097, 87_382, 104_858 + 1, 262_144, 699_051, 1_398_102, 1_677_722 + 1,
+             2_097_152, 2_796_203, 4_194_304 + 48]
+    cases = []
+    for c in range(n):
+        layout = ("planar", "readall", "split")[c % 3]
+        k = int(rng.choice([4, 6, 8, 10, 12, 16, 20]))
+        m = int(rng.choice([2, 3, 4, 8]))
+        S = int(sizes[int(rng.integers(0, len(sizes)))])
+        batch = max(2, min(4, (48 << 20) // (S * (k + m))))
+        ne = int(rng.integers(1, m + 1))
+        erase = sorted(rng.choice(k + m, size=ne, replace=False).tolist())
+        cases.append((layout, k, m, S, batch, erase, bool(c % 2)))
+    return cases
+
+
+@pytest.mark.parametrize("layout,k,m,S,batch,erase,fresh", _random_layout_cases())
+def test_random_layouts_vs_oracle(native_lib, layout, k, m, S, batch, erase, fresh):
+    """Plans on the rules alone (untuned) over seeded shapes in the planar, readall and
+    split layouts: encode against the C oracle on the first and last stripe, then the
+    erased shards rebuilt in place or (fresh) into buffers of their own, every byte back."""
+    import torch
+    from callfs_amd.device import Plan, StripeBatch, _aligned_empty
+    n = k + m
+    dev = torch.device("cuda:0")
+    sb = StripeBatch(k, m, S, batch, dev, layout=layout)
+    sb.fill_random(S ^ (k << 8) ^ m)
+    Plan.for_batch(sb).launch()
+    torch.cuda.synchronize()
+    host = sb.gather().cpu().numpy()
+    for b in {0, batch - 1}:
+        want = cref.encode([host[b, i].copy() for i in range(k)], k, m, simd=True, nthreads=4)
+        for j in range(m):
+            assert np.array_equal(host[b, k + j], want[j]), (b, j)
+    present = [i not in erase for i in range(n)]
+    if fresh:
+        out = _aligned_empty((batch, len(erase), -(-S // 64) * 64), 256, dev)
+        out.fill_(0x5A)
+        ptrs = list(sb.pointers())
+        for b in range(batch):
+            for j, i in enumerate(erase):
+                ptrs[b * n + i] = out[b, j].data_ptr()
+        dec = Plan(k, m, S, batch, ptrs, present=present)
+    else:
+        for i in erase:
+            sb.zero_shard(i)
+        dec = Plan.for_batch(sb, present=present)
+    dec.launch()
+    assert dec.corrupt_stripes() == []
+    if fresh:
+        got = out.cpu().numpy()
+        for b in range(batch):
+            for j, i in enumerate(erase):
+                assert np.array_equal(got[b, j, :S], host[b, i]), (b, i)
+    else:
+        assert np.array_equal(sb.gather().cpu().numpy(), host)
+
+
 # ---- zero-copy staging: caller buffers in rs_host_alloc memory -----------------------
 
 def _pinned(n):
