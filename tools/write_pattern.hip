@@ -38,11 +38,15 @@ struct Args {
   uint32_t rowwave; // 1: a wave's R stores go to consecutive 1 KiB pieces of one row (the
                     // block's 8R pieces dealt wave-major) instead of one piece of each row;
                     // 2: one piece of each row, each store waited for before the next
+  uint32_t split;   // 1: each block stores ONE of the R rows of its tile; the R blocks of a
+                    // tile are neighbours in launch order (the same rows in flight chip-wide
+                    // as R-row blocks, one row per block)
   uint32_t* sink;
 };
 
 __global__ __launch_bounds__(1024) void pattern(Args a) {
-  const uint32_t t = blockIdx.x;
+  const uint32_t t = a.split ? blockIdx.x / a.R : blockIdx.x;
+  const uint32_t only = a.split ? blockIdx.x % a.R : 0;
   uint32_t stripe, tile;
   if (a.order == 1) {
     const uint32_t per = a.g * a.tps, grp = t / per, r = t - grp * per;
@@ -62,6 +66,7 @@ __global__ __launch_bounds__(1024) void pattern(Args a) {
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint64_t tb = blockDim.x * 16ull;  // tile bytes per row
   for (uint32_t i = 0; i < a.R; ++i) {
+    if (a.split && i != only) continue;
     // piece f of the block's nw*R 1 KiB pieces: row f / nw, piece f % nw of the row's tile
     const uint32_t f = a.rowwave ? w * a.R + i : i * nw + w;
     const uint32_t r = f / nw, piece = f % nw;
@@ -96,10 +101,21 @@ int main(int argc, char** argv) {
     uint64_t S;
     uint32_t R, order, g, read, rowwave, bs;
     uint64_t pitch;  // 0: S
+    uint32_t split;
   };
   std::vector<V> vs;
   const uint64_t shapes[] = {1ull << 20, 2ull << 20, 6710912, 8ull << 20, 64ull << 20};
-  if (argc > 2) {
+  if (argc > 2 && argv[2][0] == 's') {
+    // one row per block against R rows per block, same rows in flight (split probe)
+    for (int rep = 0; rep < 2; ++rep)
+      for (uint64_t S : {1ull << 20, 6710912ull})
+        for (uint32_t R : {1u, 4u, 8u})
+          for (uint32_t sp : {0u, 1u}) {
+            if (R == 1 && sp) continue;
+            vs.push_back({"consecutive", S, R, 0, 0, 0, 0, 512, 0, sp});
+            vs.push_back({"G8", S, R, 1, 8, 0, 0, 512, 0, sp});
+          }
+  } else if (argc > 2) {
     const uint64_t pitches[] = {1ull << 20, (2ull << 20) + 256, 6710912, 8ull << 20};
     for (int rep = 0; rep < 2; ++rep)
       for (uint64_t P : pitches)
@@ -120,7 +136,7 @@ int main(int argc, char** argv) {
           vs.push_back({"Q8", S, R, 2, 8, 0, 0, bs, 0});
         }
   }
-  std::printf("variant,shard_bytes,pitch,rows,block,mode,GBps\n");
+  std::printf("variant,shard_bytes,pitch,rows,block,mode,split,GBps\n");
   for (const V& v : vs) {
     Args a{};
     a.base = buf;
@@ -134,13 +150,14 @@ int main(int argc, char** argv) {
     a.read = v.read;
     a.rowwave = v.rowwave;
     a.sink = sink;
-    uint32_t grid = a.tps * a.batch;
+    a.split = v.split;
+    uint32_t grid = a.tps * a.batch * (v.split ? v.R : 1);
     if (v.order == 3) {
       a.tps = 1;
       grid = static_cast<uint32_t>(total / (tb * v.R));
       a.batch = grid;
     }
-    const double bytes = static_cast<double>(grid) * v.R * tb;
+    const double bytes = static_cast<double>(grid) * (v.split ? 1 : v.R) * tb;
     for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(pattern, dim3(grid), dim3(v.bs), 0, 0, a);
     float best = 1e30f;
     for (int r = 0; r < reps; ++r) {
@@ -152,9 +169,9 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       best = ms < best ? ms : best;
     }
-    std::printf("%s,%llu,%llu,%u,%u,%s,%.0f\n", v.name, static_cast<unsigned long long>(v.S),
+    std::printf("%s,%llu,%llu,%u,%u,%s,%u,%.0f\n", v.name, static_cast<unsigned long long>(v.S),
                 static_cast<unsigned long long>(a.pitch), v.R, v.bs, v.read ? "read" : "write",
-                bytes / (best * 1e-3) / 1e9);
+                v.split, bytes / (best * 1e-3) / 1e9);
     std::fflush(stdout);
   }
   CK(hipFree(buf));
