@@ -129,6 +129,9 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
   // exactly 1 MiB apart: G2 beats G8 (RS(4,4) 128 KiB 61.2 -> 68.7, RS(8,8) 64 KiB 64.2
   // -> 67.7, RS(12,4) 64 KiB equal)
   if (stripe_stride == (1ull << 20) && tps <= 32) return TileOrder::kGroup2;
+  // (round 5: the ring that tri_rule_order leaves to more than 12 inputs up to 256 KiB runs
+  // in consecutive order; profiles/r05/tiles/)
+  if (tps <= 32 && streams - rows > 12 && rows <= 4 && !verify) return TileOrder::kConsecutive;
   if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
   // round 5, planar layout (tools/rule_sweep.sh, profiles/r05/rule/): more than 16 inputs
   // with R <= 4 on 256 KiB - 1 MiB shards run the ring faster in consecutive order
@@ -213,8 +216,16 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     return tps <= 128 ? static_cast<int>(tri_order(nibble)) : -1;
   }
   if (db && !read_only) {  // round 4, double-buffered (profiles/r04/tri_sweep3, tridb_wide)
-    // (round 5, planar: G2 for K > 16, RS(20,4) 52 KB X32 69.8 / 70.0 -> G2 72.5)
-    if (tps <= 32) return K > 16 ? g2 : x32;
+    // (round 5, planar: G2 for K > 16, RS(20,4) 52 KB X32 69.8 / 70.0 -> G2 72.5.) A sweep of
+    // shard sizes between 40 and 96 KiB (tile fills 0.0-0.8; tools/ceiling_sweep.py pinned
+    // orders, profiles/r05/tiles/) then put the ring in consecutive order ahead for K > 12
+    // whenever the pitch is not 64 KiB-aligned: K = 20 / 24 tri-G2 -> ring by 0-6 points
+    // (RS(20,4) 57,344 B 70.7 -> 73.9, 45,875 B 66.4 -> 71.3; 52,429 B equal), K = 16
+    // tri-X32 -> ring by 0.3-1.8 on 6 of 8 sizes. On power-of-two shards of at most 64 KiB
+    // tri-X32 leads the ring by 2.5-3.1 (RS(20,4) 64 KiB 76.6 vs 74.1, RS(16,4) 77.5 vs 74.4;
+    // 32 KiB equal or ahead), while at 128 KiB the ring leads by 1.7-3.9 and at 192 KiB
+    // (64 KiB-aligned) by 3-4 (rule_after*.jsonl there, K = 14..32)
+    if (tps <= 32) return K > 12 && ((S & (S - 1)) != 0 || tps > 8) ? -1 : x32;
     if (K == 6) return tps <= 1024 ? x32 : x8;
     if (tps <= 128) return K > 16 && addr_tz < 16 ? -1 : g2;
     // K >= 10 on 1-8 MiB shards at pitches that are not a power of two: the ring of three in

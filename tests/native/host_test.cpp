@@ -350,7 +350,16 @@ int main() {
     CHECK(tro(10, 4, MiB, 20) == G2);  // the nibble rule's order (G2 for the bench shape)
     // K > 16 from 256 KiB to 1 MiB: the ring on unaligned pitches, G2 on 64 KiB-aligned ones
     CHECK(tro(20, 4, 838861, 8) == -1 && tro(20, 4, MiB, 20) == G2 && tro(16, 4, 838861, 8) == G2);
-    CHECK(tro(20, 4, 52429, 8) == G2 && tro(16, 4, 65536, 16) == X32);
+    CHECK(tro(16, 4, 65536, 16) == X32 && tro(20, 4, 65536, 16) == X32);
+    // up to 256 KiB, K > 12 on shards that are not a power of two: the ring (round 5,
+    // profiles/r05/tiles/)
+    CHECK(tro(20, 4, 52429, 8) == -1 && tro(24, 4, 57344, 13) == -1 && tro(16, 4, 40960, 13) == -1);
+    CHECK(tro(16, 4, 196608, 16) == -1 && tro(32, 4, 32768, 15) == X32 && tro(20, 4, 131072, 17) == -1);
+    CHECK(tro(8, 4, 131072, 17) == X32);  // K <= 12 keep the triples
+    CHECK(tro(12, 4, 87382, 8) == X32 && tro(10, 4, 57344, 13) == X32);
+    CHECK(lds_tile_order(52429, tps_of(52429), 8, 24, 0, false, false, 4) == TileOrder::kConsecutive);
+    CHECK(lds_tile_order(65536, tps_of(65536), 16, 20, 0, false, false, 4) == TileOrder::kConsecutive);
+    CHECK(lds_tile_order(65536, tps_of(65536), 16, 16, 0, false, false, 4) == TileOrder::kGroup8);
     // read-only launches: X32 at every size above 256 KiB (RS(6,3) 16 MiB 85.7 -> 90.0)
     CHECK(tro(4, 2, 16 * MiB, 24, true, true) == X32 && tro(10, 4, MiB, 20, true, true, TileOrder::kXcd32) == X32);
     // written + Verify rows (R <= 4, early compares): K <= 4 in X32, K 5..12 up to 1 MiB
