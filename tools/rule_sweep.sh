@@ -1,7 +1,7 @@
 # The profile sweep's 33 cells (11 RS profiles x 1, 16, 64 MiB objects, ~4 GiB batches) in
 # the planar layout (the bench layout), production rule against rs_plan_tune, two passes
 # (tools/ceiling_sweep.py): the data the tile-order rule is fitted to (tile_order.hpp).
-# Usage: bash tools/rule_sweep.sh <tag> [extra ceiling_sweep args]
+# Usage: [PASSES=n] bash tools/rule_sweep.sh <tag> [extra ceiling_sweep args]
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; TAG="${1:-rule}"; shift; O="$R/gpurun_out/$TAG"; mkdir -p "$O"; cd "$R"
 A=()
@@ -12,7 +12,7 @@ for km in "4 2" "3 2" "6 3" "8 4" "10 4" "12 4" "16 4" "8 8" "10 8" "20 4" "32 8
     A+=(--shape "$k,$m,$S,$B,-,planar")
   done
 done
-for pass in 1 2; do
+for pass in $(seq 1 "${PASSES:-2}"); do
   timeout -k 10 900 python3 -u tools/ceiling_sweep.py --tune 1 --rounds 2 --only prod,tuned "${A[@]}" \
     > "$O/sweep_$pass.jsonl" 2>&1 || exit $?
   echo "pass $pass ok"
