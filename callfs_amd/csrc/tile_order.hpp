@@ -129,14 +129,13 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
   // exactly 1 MiB apart: G2 beats G8 (RS(4,4) 128 KiB 61.2 -> 68.7, RS(8,8) 64 KiB 64.2
   // -> 67.7, RS(12,4) 64 KiB equal)
   if (stripe_stride == (1ull << 20) && tps <= 32) return TileOrder::kGroup2;
-  // (round 5: the ring that tri_rule_order leaves to more than 12 inputs up to 256 KiB runs
-  // in consecutive order; profiles/r05/tiles/)
-  if (tps <= 32 && streams - rows > 12 && rows <= 4 && !verify) return TileOrder::kConsecutive;
-  if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
   // round 5, planar layout (tools/rule_sweep.sh, profiles/r05/rule/): more than 16 inputs
   // with R <= 4 on 256 KiB - 1 MiB shards run the ring faster in consecutive order
-  // (RS(20,4) 838,861 B G2 73.9 / 73.4 -> consecutive 74.9 / 74.7)
-  if (tps <= 128 && streams - rows > 16 && rows <= 4 && !verify) return TileOrder::kConsecutive;
+  // (RS(20,4) 838,861 B G2 73.9 / 73.4 -> consecutive 74.9 / 74.7); the same from 13 inputs
+  // and down to the smallest shards, where tri_rule_order leaves these launches to the ring
+  // (RS(16,4) 300,000-1,000,000 B, RS(20,4) / RS(24,4) 40-224 KiB; profiles/r05/tiles/)
+  if (tps <= 128 && streams - rows > 12 && rows <= 4 && !verify) return TileOrder::kConsecutive;
+  if (tps <= 32) return TileOrder::kGroup8;  // S <= 256 KiB
   // (round 5, planar: not for more than 16 inputs, RS(32,8) 2 MiB G2 69.3 / 69.2 ->
   // consecutive 70.4 / 70.7)
   if (tps <= 128 || (tps <= 1024 && streams >= 14 && rows >= 5 && !verify && streams - rows <= 16))
@@ -227,7 +226,12 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     // (64 KiB-aligned) by 3-4 (rule_after*.jsonl there, K = 14..32)
     if (tps <= 32) return K > 12 && ((S & (S - 1)) != 0 || tps > 8) ? -1 : x32;
     if (K == 6) return tps <= 1024 ? x32 : x8;
-    if (tps <= 128) return K > 16 && addr_tz < 16 ? -1 : g2;
+    // 256 KiB - 1 MiB (round 5, pinned orders at 9 sizes, profiles/r05/tiles/mid_band.jsonl):
+    // G2 only where the pitch is a multiple of 128 KiB (512 KiB: X32 collapses to 70-73);
+    // elsewhere X32 for K <= 12 (K = 8 / 10 tri-G2 -> tri-X32 by 1-3.4 on every size, RS(8,4)
+    // 464,531 B 75.7 -> 78.1, RS(10,4) 655,000 B 75.8 -> 78.9; K = 12 all forms within ~1)
+    // and the ring in consecutive order above (RS(16,4) 8 of 9 sizes, 832,781 B 69.2 -> 74.3)
+    if (tps <= 128) return addr_tz >= 17 ? g2 : K > 12 ? -1 : x32;
     // K >= 10 on 1-8 MiB shards at pitches that are not a power of two: the ring of three in
     // consecutive order (round 4, fourth session, tools/mid_shard_probe.sh,
     // profiles/r04/mid1/, two passes, one-block layout, tri-Q8 -> ring: RS(10,4) 1.68 MB
@@ -241,6 +245,11 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     // 77.6 / 76.9) and the ring to 8 MiB (RS(8,4) 8 MiB Q8 73.6 / 72.6 -> ring 74.2 / 75.4)
     if (K >= 10) return K <= 12 && pow2_16_32 ? q16 : -1;
     if (tps <= 256) return g2;
+    // K 7..9 from 2 to ~6.5 MiB in Q8 (round 5, pinned orders at 6 sizes,
+    // profiles/r05/tiles/r8_small_k79_mid.jsonl: ring -> tri-Q8 RS(8,4) 2.5 MB 74.0 -> 77.4,
+    // 4.39 MB 74.2 -> 78.7, 6.5 MB 74.7 -> 77.8; at 7.5 MB every triple form drops below the
+    // ring, 69.5-72.5 vs 73.7, as round 4 found at 8 MiB)
+    if (tps <= 800) return q8;
     if (tps <= 1024) return -1;
     return pow2_16_32 ? q16 : -1;
   }
@@ -263,8 +272,11 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
   // R 5..8 on shards up to 256 KiB: the rotating triples in X32 for any K (round 4,
   // planar 1 MiB objects, tools/small_r8_probe.sh, profiles/r04/smallr8/ab.jsonl: RS(32,8)
   // 32 KiB 65.9 -> 69.3, one-block layout 66.9 -> 68.7; RS(16,8) 64 KiB 69.8 -> 73.2)
-  // (round 5, planar: G2 for K <= 12, RS(8,8) 128 KiB X32 75.4 / 75.5 -> G2 76.3 / 76.5)
-  if (tps <= 32 && R >= 5 && !read_only) return K <= 12 ? g2 : x32;
+  // (round 5, planar: G2 for K <= 12 where the pitch is a multiple of 128 KiB, RS(8,8) 128 KiB
+  // X32 75.4 / 75.5 -> G2 76.3 / 76.5; elsewhere X32, which leads G2 on 23 of 30 sizes from
+  // 33 to 250 KB for K = 8..12 by up to 5 points, RS(10,8) 125,000 B 72.4 -> 77.5, RS(12,8)
+  // 75,628 B 70.6 -> 75.9; profiles/r05/tiles/r8_small_k79_mid.jsonl)
+  if (tps <= 32 && R >= 5 && !read_only) return K <= 12 && addr_tz >= 17 ? g2 : x32;
   if (K > 12) return -1;
   if (tps <= 32) return K <= 6 || R >= 5 ? x32 : -1;
   if (read_only) return x32;

@@ -274,7 +274,9 @@ int main() {
     CHECK(lds_tile_order(4 * MiB, tps_of(4 * MiB), 22, 20, 80 * MiB) == TileOrder::kGroup2);
     CHECK(lds_tile_order(4 * MiB, tps_of(4 * MiB), 22, 20, 80 * MiB, false, false, 4) ==
           TileOrder::kConsecutive);
-    CHECK(lds_tile_order(MiB, tps_of(MiB), 20, 20, 20 * MiB, false, false, 4) == TileOrder::kGroup2);
+    // (round 5: more than 12 inputs with R <= 4 up to 1 MiB run the ring in consecutive order)
+    CHECK(lds_tile_order(MiB, tps_of(MiB), 20, 20, 20 * MiB, false, false, 4) == TileOrder::kConsecutive);
+    CHECK(lds_tile_order(MiB, tps_of(MiB), 20, 16, 16 * MiB, false, false, 4) == TileOrder::kGroup2);
     // power-of-two 16 MiB shards: Q16 with 14 streams, consecutive with 6
     CHECK(lds_tile_order(16 * MiB, tps_of(16 * MiB), 24, 14, 224 * MiB) == TileOrder::kSeg16);
     CHECK(lds_tile_order(16 * MiB, tps_of(16 * MiB), 24, 6, 96 * MiB) == TileOrder::kConsecutive);
@@ -308,7 +310,8 @@ int main() {
     CHECK(tri_rule(4, 2, false, true, true, t1));     // download Verify (read-only)
     CHECK(!tri_rule(3, 2, false, false, false, t1));  // k = 3: the v_perm kernel
     CHECK(tri_rule(12, 4, false, false, false, t1));
-    CHECK(tri_rule(16, 4, false, false, false, t1));  // double-buffered from K = 6 at R <= 4
+    CHECK(tri_rule(16, 4, false, false, false, t1, 20));  // double-buffered from K = 6 at R <= 4
+    CHECK(!tri_rule(16, 4, false, false, false, tps_of(1000000), 8));  // ... the ring off 128 KiB pitches
     CHECK(!tri_rule(16, 8, false, false, false, t1)); // rotating form: K <= 12
     CHECK(tri_rule(32, 8, false, false, false, tps_of(32768)));   // ... any K up to 256 KiB
     CHECK(tri_rule(16, 8, false, false, false, tps_of(65536)));
@@ -338,6 +341,8 @@ int main() {
     // 256 KiB (K <= 12), consecutive / Q8 to 2 MiB, X32 to 8 MiB
     const int Q8 = static_cast<int>(TileOrder::kSeg8), CONS = static_cast<int>(TileOrder::kConsecutive);
     CHECK(tro(8, 4, 2 * MiB, 21) == G2 && tro(8, 4, 8 * MiB, 23) == -1);
+    CHECK(tro(8, 4, 4389515, 8) == Q8 && tro(7, 4, 2500000, 8) == Q8 && tro(9, 4, 7500000, 8) == -1);
+    CHECK(tro(10, 8, 75628, 8) == X32 && tro(12, 8, 125000, 8) == X32);
     CHECK(tro(8, 8, 131072, 17) == G2 && tro(32, 8, 32768, 15) == X32 && tro(8, 8, 2 * MiB, 21) == CONS);
     CHECK(tro(10, 8, 1677722, 8) == Q8 && tro(10, 8, 6710887, 8) == X32 && tro(8, 8, 8 * MiB, 23) == X32);
     CHECK(tro(10, 8, 16 * MiB, 8) == -1);
@@ -349,7 +354,10 @@ int main() {
     CHECK(tro(10, 4, 16 * MiB, 8) == -1 && tro(10, 4, 64 * MiB, 26) == -1);
     CHECK(tro(10, 4, MiB, 20) == G2);  // the nibble rule's order (G2 for the bench shape)
     // K > 16 from 256 KiB to 1 MiB: the ring on unaligned pitches, G2 on 64 KiB-aligned ones
-    CHECK(tro(20, 4, 838861, 8) == -1 && tro(20, 4, MiB, 20) == G2 && tro(16, 4, 838861, 8) == G2);
+    CHECK(tro(20, 4, 838861, 8) == -1 && tro(20, 4, MiB, 20) == G2 && tro(16, 4, 838861, 8) == -1);
+    // 256 KiB - 1 MiB off 128 KiB-multiple pitches: X32 for K <= 12 (round 5, mid_band.jsonl)
+    CHECK(tro(8, 4, 464531, 8) == X32 && tro(10, 4, 655000, 8) == X32 && tro(12, 4, 720000, 8) == X32);
+    CHECK(tro(8, 4, 524288, 19) == G2 && tro(12, 4, 524288, 19) == G2);
     CHECK(tro(16, 4, 65536, 16) == X32 && tro(20, 4, 65536, 16) == X32);
     // up to 256 KiB, K > 12 on shards that are not a power of two: the ring (round 5,
     // profiles/r05/tiles/)
