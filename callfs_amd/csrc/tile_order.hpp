@@ -202,14 +202,21 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     if (K <= 4) return x32;
     if (db) {  // round 4 (profiles/r04/tri_verify_ab2): G2 up to 1 MiB, X32 above
       // round 5, planar (tools/decode_rule_sweep.sh, profiles/r05/decode_rule/): up to 256 KiB
-      // the early-compare triples in G2 for K >= 7, where the ring ran (RS(10,4) 104,858 B
+      // the early-compare triples for K >= 7, where the ring ran (in G2: RS(10,4) 104,858 B
       // erase {1} 71.0 -> 75.7, {10} 72.0 -> 76.9; RS(12,4) 87,382 B {1} 69.3 -> 75.2; RS(8,4)
       // 128 KiB {1} 74.6 -> 77.6; RS(16,4) 64 KiB {1} 70.5 -> 77.3)
-      if (tps <= 32) return K <= 6 ? x32 : g2;
+      // At sizes between those cells X32 is the better single choice up to 256 KiB: G2 drops
+      // 2-7 points on 6- and 10-tile shards (RS(10,4) 75,550 B {1} 67.8 vs X32 73.9, RS(16,4)
+      // 131,072 B 69.9 vs 74.8) and leads by at most ~1.4 elsewhere (40 sizes x K = 8..16,
+      // profiles/r05/tiles/mixed_small_band.jsonl)
+      if (tps <= 32) return x32;
       if (K > 16) return -1;
       // (round 5: G2 to 2 MiB, RS(10,4) 1.68 MB {1} X32 74.7 -> G2 75.5, RS(12,4) 1.4 MB
-      // {12} 73.4 -> 74.5)
-      return tps <= 256 ? g2 : x32;
+      // {12} 73.4 -> 74.5; but below 1 MiB X32 leads G2 by 0.6-1.0 on average and up to 3.6,
+      // RS(16,4) 832,781 B {1} 72.3 -> 75.9, RS(10,4) 1,111,633 B 74.9 -> 78.2; 8 sizes x
+      // K = 6 / 10 / 16, profiles/r05/tiles/mixed_mid_band.jsonl; pitches that are multiples
+      // of 128 KiB keep G2, RS(16,4) 1 MiB {1} 76.7 with the tuner finding nothing better)
+      return tps <= 128 && addr_tz < 17 ? x32 : tps <= 256 ? g2 : x32;
     }
     if (tps <= 32) return x32;
     return tps <= 128 ? static_cast<int>(tri_order(nibble)) : -1;

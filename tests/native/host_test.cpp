@@ -374,16 +374,17 @@ int main() {
     CHECK(tro(4, 2, MiB, 20, true, false) == X32 && tro(4, 2, 4 * MiB, 22, true, false) == X32);
     CHECK(tro(10, 4, MiB, 20, true, false) == G2 && tro(10, 4, 6710887, 8, true, false) == X32);
     CHECK(tro(5, 3, 6710887, 8, true, false) == -1 && tro(20, 4, MiB, 20, true, false) == -1);
-    CHECK(tro(10, 4, 104858, 8, true, false) == G2 && tro(6, 3, 174763, 8, true, false) == X32);
+    CHECK(tro(10, 4, 104858, 8, true, false) == X32 && tro(6, 3, 174763, 8, true, false) == X32);
     // round 5, planar: mixed decodes up to 256 KiB in G2 for K >= 7; read-only launches: R 5..8
     // keep the ring (consecutive up to 256 KiB), R <= 4 take consecutive triples up to 256 KiB
     // and, with K > 12, Q8 to 1 MiB and X32 above
-    CHECK(tro(16, 4, 65536, 16, true, false) == G2 && tro(20, 4, MiB, 20, true, false) == -1);
+    CHECK(tro(16, 4, 65536, 16, true, false) == X32 && tro(20, 4, MiB, 20, true, false) == -1);
     CHECK(tro(10, 8, 104858, 8, true, true) == -1 && tro(10, 8, 1677722, 8, true, true) == -1);
     CHECK(tro(10, 4, 104858, 8, true, true) == CONS && tro(16, 4, 65536, 16, true, true) == CONS);
     CHECK(tro(16, 4, MiB, 20, true, true) == Q8 && tro(16, 4, 4 * MiB, 22, true, true) == X32);
     CHECK(tro(10, 4, 1677722, 8, true, true) == X32 && tro(10, 4, 6710887, 8, true, true) == Q8);
     CHECK(tro(10, 4, 1677722, 8, true, false) == G2 && tro(12, 4, 5592406, 8, true, false) == X32);
+    CHECK(tro(16, 4, 832781, 8, true, false) == X32 && tro(6, 3, 413283, 8, true, false) == X32);
     CHECK(lds_tile_order(104858, tps_of(104858), 8, 18, 0, true, true, 8) == TileOrder::kConsecutive);
     CHECK(tri_tunable(16, 4, false, false, false) && tri_tunable(20, 4, false, false, false) &&
           !tri_tunable(20, 8, false, false, false));  // R <= 4: the double-buffered form at any K

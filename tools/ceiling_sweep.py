@@ -121,7 +121,13 @@ def main():
         plan = enc if present is None else Plan(k, m, S, B, ptrs, present=present)
         if pin:
             from callfs_amd import _native as N
-            plan.set_orders([pin] * int(N.lib.rs_plan_groups(plan.handle)))
+            try:
+                plan.set_orders([pin] * int(N.lib.rs_plan_groups(plan.handle)))
+            except N.NativeError as e:  # not offered for this launch: reported, not run
+                print(json.dumps({"shape": spec, "skipped": f"order {pin}: {e}"}), flush=True)
+                del plan, enc, holder, fresh_buf
+                torch.cuda.empty_cache()
+                continue
         variants = {"prod": lambda: plan.launch(stream)}
         orders = None
         if a.tune:
