@@ -205,11 +205,12 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
       // the early-compare triples for K >= 7, where the ring ran (in G2: RS(10,4) 104,858 B
       // erase {1} 71.0 -> 75.7, {10} 72.0 -> 76.9; RS(12,4) 87,382 B {1} 69.3 -> 75.2; RS(8,4)
       // 128 KiB {1} 74.6 -> 77.6; RS(16,4) 64 KiB {1} 70.5 -> 77.3)
-      // At sizes between those cells X32 is the better single choice up to 256 KiB: G2 drops
-      // 2-7 points on 6- and 10-tile shards (RS(10,4) 75,550 B {1} 67.8 vs X32 73.9, RS(16,4)
-      // 131,072 B 69.9 vs 74.8) and leads by at most ~1.4 elsewhere (40 sizes x K = 8..16,
-      // profiles/r05/tiles/mixed_small_band.jsonl)
-      if (tps <= 32) return x32;
+      // Between those cells G2 collapses on shards of at most 10 tiles that are not a power of
+      // two: 2-7 points behind X32 (RS(10,4) 75,550 B {1} 67.8 vs 73.9, 45,000 B 70.0 vs 74.4;
+      // 40 sizes x K = 8..16, profiles/r05/tiles/mixed_small_band.jsonl); from 11 to 32 tiles
+      // the two tie on average and the cells above keep G2 (X32 there lost 1.5-2.7 points,
+      // profiles/r05/decode_rule/after3_x32small.jsonl)
+      if (tps <= 32) return K <= 6 || tps <= 10 ? x32 : g2;
       if (K > 16) return -1;
       // (round 5: G2 to 2 MiB, RS(10,4) 1.68 MB {1} X32 74.7 -> G2 75.5, RS(12,4) 1.4 MB
       // {12} 73.4 -> 74.5; but below 1 MiB X32 leads G2 by 0.6-1.0 on average and up to 3.6,

@@ -374,7 +374,8 @@ int main() {
     CHECK(tro(4, 2, MiB, 20, true, false) == X32 && tro(4, 2, 4 * MiB, 22, true, false) == X32);
     CHECK(tro(10, 4, MiB, 20, true, false) == G2 && tro(10, 4, 6710887, 8, true, false) == X32);
     CHECK(tro(5, 3, 6710887, 8, true, false) == -1 && tro(20, 4, MiB, 20, true, false) == -1);
-    CHECK(tro(10, 4, 104858, 8, true, false) == X32 && tro(6, 3, 174763, 8, true, false) == X32);
+    CHECK(tro(10, 4, 104858, 8, true, false) == G2 && tro(6, 3, 174763, 8, true, false) == X32);
+    CHECK(tro(10, 4, 75550, 8, true, false) == X32 && tro(16, 4, 60287, 8, true, false) == X32);
     // round 5, planar: mixed decodes up to 256 KiB in G2 for K >= 7; read-only launches: R 5..8
     // keep the ring (consecutive up to 256 KiB), R <= 4 take consecutive triples up to 256 KiB
     // and, with K > 12, Q8 to 1 MiB and X32 above
