@@ -538,7 +538,18 @@ bool wix_enabled() {
 int tri_unaligned_order(const ApplyArgs& a, uint64_t tps) {
   if (a.R > 8 || a.K < 4 || !a.in_misalign || a.out_misalign || tile_order_override() >= 0)
     return -1;
-  if (a.K > 12 && tps > 32) return -1;
+  // More than 12 inputs above 256 KiB: the realigning ring, except for R <= 4 launches that
+  // also compare rows (one-shard decodes), where the unaligned triples lead it (round 5, 40
+  // seeded object sizes in the readall layout, profiles/r05/tiles/random_readall_*: RS(16,4)
+  // 2.3 MB decode {1} 70.9 -> 73.6; its encodes split, 3.9 MB 73.4 -> 69.9)
+  const uint32_t rows = (1u << a.R) - 1;
+  const bool verify = (a.verify_mask & rows) != 0;
+  if (a.K > 12 && tps > 32 && !(a.R <= 4 && verify)) return -1;
+  // R 5..8 launches that compare rows take the realigning ring, as the aligned rule gives
+  // them the ring: the rotating unaligned triples ran 3-7 points behind it (RS(8,8) /
+  // RS(10,8) {1}, 122 KB - 24 MB: 62-64 vs 65.7-71.0; after: those 8 cells 63.7 -> 66.4
+  // on average, random_readall_dec1_after.jsonl)
+  if (a.R > 4 && verify) return -1;
   // round 5 (tools/readall_rule_sweep.sh, profiles/r05/readall_rule/): Q8 from 1 to 2 MiB,
   // X32 -> Q8: RS(10,4) 1.68 MB 74.9 -> 76.6, RS(12,4) 1.4 MB 75.1 -> 76.3, RS(8,8) 2 MiB
   // 75.0 -> 76.3, RS(10,8) 1.68 MB 70.4 -> 71.7
