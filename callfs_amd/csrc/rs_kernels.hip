@@ -589,6 +589,12 @@ int tri_index(TileOrder o) {
   }
 }
 bool takes_realign(const ApplyArgs& a) {
+  // (round 5: R 5..8 launches with misaligned inputs, aligned outputs and compared rows run
+  // the plain ring on unaligned loads 3.2-4.5 points ahead of the realigning form, RS(8,8)
+  // 23.8 MB {1} readall 67.8 -> 72.3, RS(10,8) 161,009 B 62.1 -> 66.6;
+  // profiles/r05/tiles/random_readall_dec1_after.jsonl)
+  const uint32_t rows = (1u << a.R) - 1;
+  if (a.R > 4 && (a.verify_mask & rows) != 0 && a.in_misalign && !a.out_misalign) return false;
   return can_realign(a) && ((a.in_misalign | a.out_misalign) & 1u) && !takes_tri(a);
 }
 // the 64-vector realigning form: misaligned inputs, every output 16-B aligned
