@@ -545,8 +545,9 @@ int tri_unaligned_order(const ApplyArgs& a, uint64_t tps) {
   const uint32_t rows = (1u << a.R) - 1;
   const bool verify = (a.verify_mask & rows) != 0;
   if (a.K > 12 && tps > 32 && !(a.R <= 4 && verify)) return -1;
-  // R 5..8 launches that compare rows take the realigning ring, as the aligned rule gives
-  // them the ring: the rotating unaligned triples ran 3-7 points behind it (RS(8,8) /
+  // R 5..8 launches that compare rows take a ring, as the aligned rule gives them the ring
+  // (the plain one on unaligned loads, takes_realign): the rotating unaligned triples ran
+  // 3-7 points behind the ring forms (RS(8,8) /
   // RS(10,8) {1}, 122 KB - 24 MB: 62-64 vs 65.7-71.0; after: those 8 cells 63.7 -> 66.4
   // on average, random_readall_dec1_after.jsonl)
   if (a.R > 4 && verify) return -1;
