@@ -21,8 +21,8 @@ LIB_AB = os.path.join(HERE, "libcallfs_rs_ab.so")
 # kernel-resource-usage remarks), checked by tests/test_kernel_resources.py: the LDS
 # kernel's speed depends on its waves per SIMD.
 RESOURCES = os.path.join(HERE, "kernel_resources.json")
-SOURCES = ["rs_kernels.hip", "sha256.hip", "rs_capi.cpp"]
-HEADERS = ["rs_kernels.hpp", "rs_apply.hpp", "tile_order.hpp", "gf256.hpp", "copy_pool.hpp", "dispatch.hpp", "sha256.hpp", os.path.join("..", "..", "include", "callfs_rs.h")]
+SOURCES = ["rs_kernels.hip", "sha256.hip", "rs_capi.cpp", "bitslice.cpp"]
+HEADERS = ["bitslice.hpp", "bitslice_gen.hpp", "rs_kernels.hpp", "rs_apply.hpp", "tile_order.hpp", "gf256.hpp", "copy_pool.hpp", "dispatch.hpp", "sha256.hpp", os.path.join("..", "..", "include", "callfs_rs.h")]
 ARCH = os.environ.get("CALLFS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -78,8 +78,9 @@ def build(force: bool = False, extra_flags=None, ab: bool = False) -> str:
             raise subprocess.CalledProcessError(r.returncode, cmd)
         objs.append(obj)
     tmp = lib + ".tmp"
-    subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp],
-                   check=True)
+    # libhiprtc: the bit-sliced kernels are compiled at plan time (csrc/bitslice.cpp)
+    subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-lhiprtc",
+                    "-Wl,-rpath,/opt/rocm/lib", "-o", tmp], check=True)
     os.replace(tmp, lib)
     for o in objs:
         os.remove(o)

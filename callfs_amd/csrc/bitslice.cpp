@@ -1,0 +1,304 @@
+// Runtime of the bit-sliced kernels (bitslice.hpp): hiprtc compile, code-object cache,
+// per-device modules, the background compile worker and the launch.
+#include "bitslice.hpp"
+
+#include <hip/hip_ext.h>
+#include <hip/hiprtc.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <thread>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <cstddef>
+
+namespace callfs {
+namespace bs {
+
+static_assert(sizeof(Args) == 56 && offsetof(Args, nvec) == 24 && offsetof(Args, order) == 52,
+              "Args: the layout args_decl() declares to the generated source");
+
+namespace {
+
+uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+// gfx950 (or the device's own gfx name when one is current); CALLFS_OFFLOAD_ARCH overrides.
+std::string target_arch() {
+  if (const char* e = std::getenv("CALLFS_OFFLOAD_ARCH")) return e;
+  int dev = -1;
+  hipDeviceProp_t p;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) {
+    std::string a = p.gcnArchName;
+    const size_t colon = a.find(':');
+    if (colon != std::string::npos) a.resize(colon);
+    if (!a.empty()) return a;
+  }
+  return "gfx950";
+}
+
+// On-disk cache of code objects: CALLFS_RS_JIT_CACHE (a directory; "0" turns it off), else
+// $XDG_CACHE_HOME/callfs_rs or $HOME/.cache/callfs_rs. Files are written whole and renamed
+// into place, so concurrent processes never read a partial one.
+std::string cache_dir() {
+  const char* e = std::getenv("CALLFS_RS_JIT_CACHE");
+  if (e) return std::strcmp(e, "0") == 0 ? std::string() : std::string(e);
+  if (const char* x = std::getenv("XDG_CACHE_HOME")) return std::string(x) + "/callfs_rs";
+  if (const char* h = std::getenv("HOME")) return std::string(h) + "/.cache/callfs_rs";
+  return std::string();
+}
+
+bool read_file(const std::string& path, std::vector<char>& out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+  return !out.empty();
+}
+
+void write_file(const std::string& dir, const std::string& path, const std::vector<char>& data) {
+  if (dir.empty()) return;
+  // mkdir -p of the cache directory (two levels at most: <cache>/callfs_rs)
+  std::string acc;
+  std::stringstream ss(dir);
+  std::string part;
+  if (!dir.empty() && dir[0] == '/') acc = "/";
+  while (std::getline(ss, part, '/')) {
+    if (part.empty()) continue;
+    acc += part + "/";
+    (void)::mkdir(acc.c_str(), 0755);
+  }
+  const std::string tmp = path + ".tmp." + std::to_string(::getpid());
+  {
+    std::ofstream f(tmp, std::ios::binary);
+    if (!f) return;
+    f.write(data.data(), static_cast<std::streamsize>(data.size()));
+    if (!f) return;
+  }
+  (void)std::rename(tmp.c_str(), path.c_str());
+}
+
+}  // namespace
+
+// One background thread compiles queued kernels in order. It is joined at exit after the
+// compile in flight (queued ones are dropped), so no hiprtc call outlives the process's
+// static teardown.
+class Worker {
+ public:
+  static Worker& get() {
+    static Worker w;
+    return w;
+  }
+  void push(const std::shared_ptr<Kernel>& k) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+    q_.push_back(k);
+    cv_.notify_one();
+  }
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+      q_.clear();
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::shared_ptr<Kernel> k;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+        if (stop_) return;
+        k = q_.front().lock();
+        q_.pop_front();
+      }
+      if (k) k->compile_now();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::weak_ptr<Kernel>> q_;
+  std::thread th_;
+  bool stop_ = false;
+};
+
+Mode mode() {
+  static const Mode m = [] {
+    const char* e = std::getenv("CALLFS_RS_BITSLICE");
+    if (!e || !*e) return Mode::kAuto;
+    if (!std::strcmp(e, "0") || !std::strcmp(e, "off")) return Mode::kOff;
+    if (!std::strcmp(e, "sync")) return Mode::kSync;
+    return Mode::kAuto;
+  }();
+  return m;
+}
+
+Kernel::Kernel(int K, int R, const uint8_t* coef) : net_(build_network(K, R, coef)) {}
+
+Kernel::State Kernel::state() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return state_;
+}
+
+void Kernel::compile_async() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (state_ != State::kIdle) return;
+    state_ = State::kQueued;
+  }
+  Worker::get().push(shared_from_this());
+}
+
+bool Kernel::compile_now() {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    if (state_ == State::kReady) return true;
+    if (state_ == State::kFailed) return false;
+    if (state_ == State::kCompiling) {
+      cv_.wait(lk);
+      continue;
+    }
+    compile_locked(lk);
+  }
+}
+
+void Kernel::compile_locked(std::unique_lock<std::mutex>& lk) {
+  state_ = State::kCompiling;
+  const Network net = net_;
+  const GenOptions opt = opt_;
+  lk.unlock();
+  const auto t0 = std::chrono::steady_clock::now();
+  const std::string arch = target_arch();
+  const std::string src = kernel_source(net, "rs_bs", opt, sizeof(Args));
+  int ver_major = 0, ver_minor = 0;
+  (void)hiprtcVersion(&ver_major, &ver_minor);
+  const std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17",
+                                         "-fno-gpu-rdc"};
+  std::string keytxt = src + arch + std::to_string(ver_major) + "." + std::to_string(ver_minor);
+  for (const auto& o : opts) keytxt += o;
+  char name[64];
+  std::snprintf(name, sizeof name, "bs-%016llx.co", static_cast<unsigned long long>(fnv1a(keytxt)));
+  const std::string dir = cache_dir();
+  const std::string path = dir.empty() ? std::string() : dir + "/" + name;
+  std::vector<char> code;
+  std::string err;
+  if (path.empty() || !read_file(path, code)) {
+    code.clear();
+    hiprtcProgram p = nullptr;
+    if (hiprtcCreateProgram(&p, src.c_str(), "rs_bs.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+      err = "hiprtcCreateProgram failed";
+    } else {
+      std::vector<const char*> o;
+      for (const auto& s : opts) o.push_back(s.c_str());
+      const hiprtcResult r = hiprtcCompileProgram(p, static_cast<int>(o.size()), o.data());
+      if (r != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        (void)hiprtcGetProgramLogSize(p, &n);
+        std::string log(n, '\0');
+        if (n) (void)hiprtcGetProgramLog(p, &log[0]);
+        err = std::string("hiprtc: ") + hiprtcGetErrorString(r) + "\n" + log;
+      } else {
+        size_t n = 0;
+        if (hiprtcGetCodeSize(p, &n) == HIPRTC_SUCCESS && n) {
+          code.resize(n);
+          if (hiprtcGetCode(p, code.data()) != HIPRTC_SUCCESS) code.clear();
+        }
+        if (code.empty()) err = "hiprtc: no code object";
+      }
+      (void)hiprtcDestroyProgram(&p);
+    }
+    if (!code.empty() && !path.empty()) write_file(dir, path, code);
+  }
+  const double secs =
+      std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  lk.lock();
+  compile_s_ = secs;
+  if (code.empty()) {
+    error_ = err;
+    state_ = State::kFailed;
+    if (std::getenv("CALLFS_RS_BITSLICE_LOG"))
+      std::fprintf(stderr, "callfs_rs bitslice K=%d R=%d: %s\n", net.K, net.R, err.c_str());
+  } else {
+    code_ = std::move(code);
+    state_ = State::kReady;
+    if (std::getenv("CALLFS_RS_BITSLICE_LOG"))
+      std::fprintf(stderr, "callfs_rs bitslice K=%d R=%d: %zu B code object in %.2f s\n", net.K,
+                   net.R, code_.size(), secs);
+  }
+  cv_.notify_all();
+}
+
+hipFunction_t Kernel::function(int device, bool wait) {
+  if (device < 0 || device >= kMaxDevices) return nullptr;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (fn_[device]) return fn_[device];
+  }
+  if (wait) {
+    if (!compile_now()) return nullptr;
+  } else if (state() != State::kReady) {
+    compile_async();
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  if (fn_[device]) return fn_[device];
+  if (state_ != State::kReady) return nullptr;
+  hipModule_t m = nullptr;
+  hipFunction_t f = nullptr;
+  if (hipModuleLoadData(&m, code_.data()) != hipSuccess) return nullptr;
+  if (hipModuleGetFunction(&f, m, "rs_bs") != hipSuccess) {
+    (void)hipModuleUnload(m);
+    return nullptr;
+  }
+  int regs = 0;
+  if (hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f) == hipSuccess) vgprs_ = regs;
+  mod_[device] = m;
+  fn_[device] = f;
+  return f;
+}
+
+std::shared_ptr<Kernel> kernel_for(int K, int R, const uint8_t* coef) {
+  // never destroyed: modules stay loaded until the process ends (unloading them from a
+  // static destructor could run after the HIP runtime's own teardown)
+  static auto* mu = new std::mutex;
+  static auto* map = new std::map<std::string, std::shared_ptr<Kernel>>;
+  std::string key(reinterpret_cast<const char*>(&K), sizeof K);
+  key.append(reinterpret_cast<const char*>(&R), sizeof R);
+  key.append(reinterpret_cast<const char*>(coef), static_cast<size_t>(K) * R);
+  std::lock_guard<std::mutex> g(*mu);
+  auto it = map->find(key);
+  if (it != map->end()) return it->second;
+  auto k = std::make_shared<Kernel>(K, R, coef);
+  map->emplace(key, k);
+  return k;
+}
+
+hipError_t launch(hipFunction_t fn, const Args& a, uint32_t tiles, hipStream_t stream,
+                  hipEvent_t ev_start, hipEvent_t ev_stop) {
+  Args args = a;
+  size_t size = sizeof args;
+  void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                    HIP_LAUNCH_PARAM_END};
+  if (ev_start || ev_stop)
+    return hipExtModuleLaunchKernel(fn, tiles * static_cast<uint32_t>(kBlockThreads), 1, 1,
+                                    kBlockThreads, 1, 1, 0, stream, nullptr, config, ev_start,
+                                    ev_stop, 0);
+  return hipModuleLaunchKernel(fn, tiles, 1, 1, kBlockThreads, 1, 1, 0, stream, nullptr, config);
+}
+
+}  // namespace bs
+}  // namespace callfs

@@ -1,0 +1,76 @@
+// Bit-sliced GF(2^8) kernels compiled at plan time: the runtime around
+// bitslice_gen.hpp. One Kernel per distinct coefficient block (K inputs x R rows), compiled
+// once per process by hiprtc for gfx950 (and kept in an on-disk cache of code objects),
+// loaded into each device on first use.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "bitslice_gen.hpp"
+#include "dispatch.hpp"
+
+namespace callfs {
+namespace bs {
+
+class Kernel : public std::enable_shared_from_this<Kernel> {
+ public:
+  enum class State { kIdle, kQueued, kCompiling, kReady, kFailed };
+  Kernel(int K, int R, const uint8_t* coef);
+  Kernel(const Kernel&) = delete;
+  Kernel& operator=(const Kernel&) = delete;
+
+  int K() const { return net_.K; }
+  int R() const { return net_.R; }
+  State state() const;
+  // Queues the compile on the background worker (no-op once queued or done).
+  void compile_async();
+  // Compiles on the calling thread if nobody has (waits for a compile in flight); true when
+  // the code object exists.
+  bool compile_now();
+  // The kernel for HIP device `device` (the caller's current device), loading the module on
+  // first use; null when not compiled or the load failed. wait: compile first if needed.
+  hipFunction_t function(int device, bool wait);
+  // Compiler-reported resources of the code object (0 before it exists).
+  int vgprs() const { return vgprs_; }
+  double compile_seconds() const { return compile_s_; }
+  const std::string& error() const { return error_; }
+
+ private:
+  friend class Worker;
+  void compile_locked(std::unique_lock<std::mutex>& lk);
+
+  Network net_;
+  GenOptions opt_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  State state_ = State::kIdle;
+  std::vector<char> code_;
+  std::string error_;
+  int vgprs_ = 0;
+  double compile_s_ = 0;
+  hipModule_t mod_[kMaxDevices] = {};
+  hipFunction_t fn_[kMaxDevices] = {};
+};
+
+// The process-wide kernel for a coefficient block (coef: [R][K] row-major); never null.
+std::shared_ptr<Kernel> kernel_for(int K, int R, const uint8_t* coef);
+
+// CALLFS_RS_BITSLICE: 0 = never, 1 / auto (default) = the rule's launch groups once their
+// kernel is compiled (plans compile it at creation), sync = compile on first use and wait.
+enum class Mode { kOff, kAuto, kSync };
+Mode mode();
+
+// Launches rs_bs over `tiles` tiles starting at a.t_base (kBlockThreads threads per tile);
+// ev_start / ev_stop as hipExtModuleLaunchKernel takes them.
+hipError_t launch(hipFunction_t fn, const Args& a, uint32_t tiles, hipStream_t stream,
+                  hipEvent_t ev_start, hipEvent_t ev_stop);
+
+}  // namespace bs
+}  // namespace callfs

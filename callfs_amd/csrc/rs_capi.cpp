@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/callfs_rs.h"
+#include "bitslice.hpp"
 #include "copy_pool.hpp"
 #include "dispatch.hpp"
 #include "gf256.hpp"
@@ -80,6 +81,8 @@ struct Group {
   uint32_t verify_mask = 0;   // bit r: compare row r (Verify) instead of storing it
   std::vector<uint32_t> tabs; // [k][R][5] v_perm tables
   std::vector<uint8_t> ltabs;  // [k][32][W] LDS nibble tables (used for R >= 5)
+  // the group's bit-sliced kernel (bitslice.hpp; compiled on demand), R >= kBitsliceMinRows
+  std::shared_ptr<bs::Kernel> bsk;
 };
 
 struct Tables {
@@ -119,6 +122,12 @@ std::shared_ptr<const Tables> build_tables(int k, int m, const uint8_t* present,
       uint8_t col[kMaxRowsPerLaunch] = {0};
       for (int r = 0; r < R; ++r) col[r] = dp.rows.at(g0 + r, i);
       nibble_tables(col, R, &g.ltabs[static_cast<size_t>(i) * per_shard]);
+    }
+    if (R >= kBitsliceMinRows && bs::mode() != bs::Mode::kOff) {
+      std::vector<uint8_t> coef(static_cast<size_t>(R) * k);
+      for (int r = 0; r < R; ++r)
+        for (int i = 0; i < k; ++i) coef[static_cast<size_t>(r) * k + i] = dp.rows.at(g0 + r, i);
+      g.bsk = bs::kernel_for(k, R, coef.data());
     }
     t->groups.push_back(std::move(g));
   }
@@ -419,6 +428,7 @@ ApplyArgs group_args(const Tables& t, const MetaLayout& L, size_t gi, int batch,
   a.stripe_stride = hint.stripe_stride;
   a.in_misalign = hint.in_misalign;
   a.out_misalign = hint.out_misalign;
+  a.bs = g.bsk.get();
   return a;
 }
 

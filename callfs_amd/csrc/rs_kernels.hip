@@ -12,6 +12,7 @@
 
 #include <hip/hip_ext.h>
 
+#include "bitslice.hpp"
 #include "dispatch.hpp"
 #include "rs_apply.hpp"
 #include "tile_order.hpp"
@@ -625,7 +626,54 @@ int realign_order_index(int order) {
 
 }  // namespace
 
-std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
+namespace {
+std::vector<int> nibble_candidates(const ApplyArgs& a0, bool every_instance);
+bool can_bitslice(const ApplyArgs& a);
+
+// The bit-sliced kernel's orders: launch groups of kBitsliceMinRows or more
+// rows whose plan carries a kernel handle (ApplyArgs::bs), unless CALLFS_RS_BITSLICE=0.
+bool can_bitslice(const ApplyArgs& a) {
+  return a.bs && a.R >= kBitsliceMinRows && a.K >= 1 && a.S >= 16 && bs::mode() != bs::Mode::kOff;
+}
+// The rule's bit-sliced launches and their order (tile_order.hpp bitslice_rule)
+bool takes_bitslice(const ApplyArgs& a) {
+  return can_bitslice(a) &&
+         bitslice_rule(a.K, a.R, (a.S / 16 + bs::kTileVecs - 1) / bs::kTileVecs,
+                       (a.in_misalign | a.out_misalign) != 0);
+}
+TileOrder bitslice_rule_order(const ApplyArgs& a) {
+  return bitslice_tile_order((a.S / 16 + bs::kTileVecs - 1) / bs::kTileVecs);
+}
+// bs::Args::order of a TileOrder (-1: no generated form)
+int bitslice_order(TileOrder o) {
+  switch (o) {
+    case TileOrder::kConsecutive: return 0;
+    case TileOrder::kSeg8: return 1;
+    case TileOrder::kXcd32: return 2;
+    case TileOrder::kGroup2: return 3;
+    default: return -1;
+  }
+}
+}  // namespace
+
+std::vector<int> order_candidates(const ApplyArgs& a, bool every_instance) {
+  std::vector<int> c = nibble_candidates(a, every_instance);
+  if (!c.empty() && can_bitslice(a)) {
+    const uint64_t tps = (a.S / 16 + bs::kTileVecs - 1) / bs::kTileVecs;
+    auto add = [&c](TileOrder o) {
+      const int v = kOrderBitslice + static_cast<int>(o);
+      if (std::find(c.begin(), c.end(), v) == c.end()) c.push_back(v);
+    };
+    add(TileOrder::kConsecutive);
+    add(TileOrder::kXcd32);
+    if (tps <= 64 || every_instance) add(TileOrder::kGroup2);
+    if (tps >= 64 || every_instance) add(TileOrder::kSeg8);
+  }
+  return c;
+}
+
+namespace {
+std::vector<int> nibble_candidates(const ApplyArgs& a0, bool every_instance) {
   ApplyArgs a = a0;
   a.nvec = a.S / 16;
   std::vector<int> c;
@@ -728,12 +776,76 @@ std::vector<int> order_candidates(const ApplyArgs& a0, bool every_instance) {
   if (tps > 1024) add(TileOrder::kSeg16);
   return c;
 }
+}  // namespace
+
+namespace {
+// One launch of the group's bit-sliced kernel in tile order `ord` (plus the byte kernel for
+// the S % 16 tail). Returns false, launching nothing, when the kernel is not compiled yet and
+// `wait` is false (the caller then runs the nibble-table kernel); with `wait` a kernel that
+// cannot be compiled or loaded returns true with *err set.
+bool launch_bitslice(ApplyArgs a, hipStream_t stream, TileOrder ord, LaunchEvents ev, bool wait,
+                     hipError_t* err) {
+  *err = hipSuccess;
+  const int bo = bitslice_order(ord);
+  if (!can_bitslice(a) || bo < 0) {
+    if (wait) *err = hipErrorInvalidValue;
+    return wait;
+  }
+  int device = -1;
+  if (hipGetDevice(&device) != hipSuccess) {
+    *err = hipErrorInvalidDevice;
+    return true;
+  }
+  auto* k = static_cast<bs::Kernel*>(const_cast<void*>(a.bs));
+  const hipFunction_t fn = k->function(device, wait);
+  if (!fn) {
+    if (wait) *err = hipErrorNoBinaryForGpu;
+    return wait;
+  }
+  bs::Args b{};
+  b.in_tab = a.in_tab;
+  b.out_tab = a.out_tab;
+  b.status = a.status;
+  b.nvec = a.S / 16;
+  b.tps = static_cast<uint32_t>((b.nvec + bs::kTileVecs - 1) / bs::kTileVecs);
+  b.ntiles = b.tps * static_cast<uint32_t>(a.batch);
+  b.verify_mask = a.verify_mask;
+  b.status_stride = a.status_stride;
+  b.order = bo;
+  const bool tail_after = b.nvec * 16 < a.S;
+  launch_sliced(b.ntiles, a.K + a.R, a, [&](uint32_t blocks, bool first, bool last) {
+    b.t_base = a.t_base;
+    const hipError_t e = bs::launch(fn, b, blocks, stream, first ? ev.start : nullptr,
+                                    last && !tail_after ? ev.stop : nullptr);
+    if (e != hipSuccess && *err == hipSuccess) *err = e;
+  });
+  if (*err != hipSuccess) return true;
+  if (tail_after) {
+    const uint64_t tail0 = b.nvec * 16;
+    const unsigned gy = static_cast<unsigned>(std::min(a.batch, 65535));
+    const uint64_t gx = (a.S - tail0 + kBlock - 1) / kBlock;
+    dispatch(kByte[a.R - 1], dim3(static_cast<unsigned>(gx), gy), dim3(kBlock), 0, stream, ev,
+             /*first=*/false, /*last=*/true, a, tail0);
+    *err = hipGetLastError();
+  }
+  return true;
+}
+}  // namespace
 
 hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int order,
                         LaunchEvents ev) {
   if (a.R < 1 || a.R > kMaxRowsPerLaunch || a.K < 1 || a.K > kMaxK || a.batch < 1)
     return hipErrorInvalidValue;
   if (a.S == 0) return hipSuccess;
+  // the bit-sliced kernel: a pinned kOrderBitslice order waits for its compile; the rule's
+  // choice runs it once compiled and the nibble-table kernel until then
+  if (!bytes_only && (order >= kOrderBitslice || (order < 0 && takes_bitslice(a)))) {
+    const bool pinned = order >= kOrderBitslice;
+    const TileOrder bo = pinned ? static_cast<TileOrder>(order - kOrderBitslice) : bitslice_rule_order(a);
+    hipError_t e = hipSuccess;
+    if (launch_bitslice(a, stream, bo, ev, pinned || bs::mode() == bs::Mode::kSync, &e)) return e;
+    order = -1;
+  }
   // (A/B) the double-buffered triples in G4 / G8: the nibble instances' G8 order underneath
   int tdg = -1;
   if (order >= kOrderTriDbG) {
@@ -961,7 +1073,8 @@ hipError_t launch_ceiling(ApplyArgs a, hipStream_t stream, int order, int mode, 
   a.nvec = a.S / 16;
   if (a.nvec == 0) return hipSuccess;
   a.tail_in_vec = a.nvec * 16 < a.S ? tail_code(a.nvec, LdsPolicy::TILE_VECS, LdsPolicy::BS) : 0u;
-  if (order >= kOrderTriDbG) order = static_cast<int>(TileOrder::kGroup8);  // (A/B forms:
+  if (order >= kOrderBitslice) order -= kOrderBitslice;  // (bit-sliced: its tile order)
+  else if (order >= kOrderTriDbG) order = static_cast<int>(TileOrder::kGroup8);  // (A/B forms:
   else if (order >= kOrderDma) order -= kOrderDma;                          //  their tile order)
   else if (order >= kOrderRealign64) order = order - kOrderRealign64 + kOrderRealign;
   else if (order >= kOrderRealignTri) order = order - kOrderRealignTri + kOrderRealign;

@@ -60,6 +60,9 @@ struct ApplyArgs {
   // (no separate byte-kernel launch): (tile << 2) | (last wave << 1) | 1, the tile of each
   // stripe and the wave (0 or the block's last) that take it (rs_apply.hpp tail_lane)
   uint32_t tail_in_vec;
+  // host-side handle of the launch group's bit-sliced kernel (bitslice.hpp bs::Kernel, compiled
+  // at plan time for this coefficient block) or null; the device kernels never read it
+  const void* bs;
 };
 
 // One-dispatch small host calls (rs_apply_small): stripe b's shard i lives at
@@ -137,6 +140,10 @@ constexpr int kOrderDma = 192;
 // (kOrderTriDbG + 0 / 1: R <= 4, K >= 6 double-buffered triples with the tiles of 4 / 8 stripes
 // interleaved (G4 / G8); A/B build)
 constexpr int kOrderTriDbG = 224;
+// (kOrderBitslice + consecutive / G2 / Q8 / X32: the launch group's bit-sliced kernel,
+// ApplyArgs::bs; R >= kBitsliceMinRows)
+constexpr int kOrderBitslice = 256;
+constexpr int kBitsliceMinRows = 5;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the

@@ -70,6 +70,17 @@ CALLFS_HD inline uint32_t block_tile(uint32_t b, uint32_t nblocks) {
 enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16, kXcd8, kXcd32 };
 constexpr int kTileOrders = 7;
 
+// Launch groups that take the bit-sliced kernel (rs_kernels.hip launch_bitslice, DESIGN.md
+// §5.7) once it is compiled: none until measured.
+inline bool bitslice_rule(int K, int R, uint64_t tps, bool misaligned) {
+  (void)K; (void)R; (void)tps; (void)misaligned;
+  return false;
+}
+// ... and their tile order
+inline TileOrder bitslice_tile_order(uint64_t tps) {
+  return tps >= 128 ? TileOrder::kSeg8 : TileOrder::kConsecutive;
+}
+
 // Tile order for R <= 8 (Policy::ORD; tools/kbench.hip KB_ORD, tools/order_sweep.sh,
 // 5-15 rounds, % of 8 TB/s, DESIGN.md "Tile order"). Neighbouring blocks normally take
 // neighbouring column tiles of one stripe (consecutive). For small shards it pays to

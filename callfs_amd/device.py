@@ -222,7 +222,8 @@ class Plan:
                    100: "tri-q16", 101: "tri-x8", 102: "tri-x32", 128: "realign-tri", 133: "realign-tri-x8",
                    134: "realign-tri-x32", 160: "realign64", 165: "realign64-x8",
                    166: "realign64-x32", 192: "dma", 194: "dma-g2", 195: "dma-q8",
-                   198: "dma-x32", 224: "tridb-g4", 225: "tridb-g8"}
+                   198: "dma-x32", 224: "tridb-g4", 225: "tridb-g8", 256: "bs", 258: "bs-g2",
+                   259: "bs-q8", 262: "bs-x32"}
 
     def tune(self, reps: int = 5, stream: Optional[torch.cuda.Stream] = None) -> list:
         """rs_plan_tune: time each launch group in every tile order its kernel offers
