@@ -5,6 +5,7 @@ next to this file so it travels to the GPU box with the repo snapshot.
 """
 from __future__ import annotations
 
+import concurrent.futures
 import hashlib
 import json
 import os
@@ -61,7 +62,8 @@ def build(force: bool = False, extra_flags=None, ab: bool = False) -> str:
     if ab:
         flags.append("-DCALLFS_RS_AB_INSTANCES=1")
     kernels = []
-    for src in SOURCES:
+
+    def compile_one(src):
         obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + (".ab.o" if ab else ".o"))
         cmd = [_hipcc(), *flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if src.endswith(".cpp"):
@@ -69,7 +71,12 @@ def build(force: bool = False, extra_flags=None, ab: bool = False) -> str:
             cmd.insert(2, "hip")
         else:
             cmd.append("-Rpass-analysis=kernel-resource-usage")
-        r = subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
+        return src, obj, cmd, subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
+
+    # the sources compile independently: in parallel (rs_kernels.hip dominates)
+    with concurrent.futures.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        results = list(ex.map(compile_one, SOURCES))
+    for src, obj, cmd, r in results:
         kernels += _parse_resource_remarks(r.stderr)
         other = [ln for ln in r.stderr.splitlines() if "kernel-resource-usage" not in ln]
         if r.returncode != 0 or any("error" in ln or "warning" in ln for ln in other):

@@ -5,6 +5,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -147,7 +148,16 @@ Mode mode() {
   return m;
 }
 
-Kernel::Kernel(int K, int R, const uint8_t* coef) : net_(build_network(K, R, coef)) {}
+Kernel::Kernel(int K, int R, const uint8_t* coef) : net_(build_network(K, R, coef)) {
+  // development knobs (tools/bs_probe.py): prefetch depth and the waves-per-SIMD floor
+  if (const char* e = std::getenv("CALLFS_RS_BS_PREFETCH")) opt_.prefetch = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("CALLFS_RS_BS_WAVES")) opt_.min_waves = std::max(1, std::min(8, std::atoi(e)));
+}
+
+Kernel::~Kernel() {
+  for (int d = 0; d < kMaxDevices; ++d)
+    if (mod_[d]) (void)hipModuleUnload(mod_[d]);
+}
 
 Kernel::State Kernel::state() const {
   std::lock_guard<std::mutex> g(mu_);
@@ -282,6 +292,11 @@ std::shared_ptr<Kernel> kernel_for(int K, int R, const uint8_t* coef) {
   std::lock_guard<std::mutex> g(*mu);
   auto it = map->find(key);
   if (it != map->end()) return it->second;
+  // bounded like the coefficient-table cache (rs_capi.cpp TableCache): past kCap entries the
+  // kernels no table set or compile holds any more are dropped (their modules unloaded)
+  constexpr size_t kCap = 1024;
+  if (map->size() >= kCap)
+    for (auto i = map->begin(); i != map->end();) i = i->second.use_count() == 1 ? map->erase(i) : std::next(i);
   auto k = std::make_shared<Kernel>(K, R, coef);
   map->emplace(key, k);
   return k;

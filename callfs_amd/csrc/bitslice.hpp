@@ -23,6 +23,7 @@ class Kernel : public std::enable_shared_from_this<Kernel> {
  public:
   enum class State { kIdle, kQueued, kCompiling, kReady, kFailed };
   Kernel(int K, int R, const uint8_t* coef);
+  ~Kernel();
   Kernel(const Kernel&) = delete;
   Kernel& operator=(const Kernel&) = delete;
 

@@ -52,7 +52,7 @@ struct Args {
   uint32_t t_base;               // first tile of this dispatch (sliced grids)
   uint32_t verify_mask;          // bit r: compare row r instead of storing it
   int status_stride;
-  int order;                     // tile order: 0 consecutive, 1 Q8, 2 X32, 3 G2
+  int order;                     // tile order: 0 consecutive, 1 Q8, 2 X32, 3 G2, 4 X8, 5 G8, 6 Q16
 };
 
 inline const char* args_decl() {
@@ -257,22 +257,25 @@ __device__ __forceinline__ void ld32(u32 (&x)[8], const unsigned char* p, u64 va
   x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
 }
 __device__ __forceinline__ void map_tile(const Args& a, u32 b, u32& stripe, u32& tile) {
+  // a.order: 0 consecutive, 1 Q8, 2 X32, 3 G2, 4 X8, 5 G8, 6 Q16 (tile_order.hpp map_tile /
+  // block_tile: the same bijections the nibble-table kernels use)
   u32 t = a.t_base + b;
-  if (a.order == 2) {  // X32: each XCD takes runs of 32 neighbouring tiles (tile_order.hpp block_tile<11>)
-    const u32 G = 256u, nb = gridDim.x;
-    if (b < nb / G * G) { const u32 g = b / G, r = b - g * G; t = a.t_base + g * G + (r & 7u) * 32u + (r >> 3); }
+  if (a.order == 2 || a.order == 4) {  // X32 / X8: each XCD takes runs of J neighbouring tiles
+    const u32 J = a.order == 2 ? 32u : 8u, G = 8u * J, nb = gridDim.x;
+    if (b < nb / G * G) { const u32 g = b / G, r = b - g * G; t = a.t_base + g * G + (r & 7u) * J + (r >> 3); }
   }
-  if (a.order == 3) {  // G2: the same tile of 2 stripes on neighbouring blocks
-    const u32 per = 2u * a.tps, g = t / per, r = t - g * per;
-    const u32 bt = a.ntiles / a.tps, gsz = bt - g * 2u < 2u ? bt - g * 2u : 2u;
-    tile = r / gsz; stripe = g * 2u + (r - tile * gsz);
+  if (a.order == 3 || a.order == 5) {  // G2 / G8: the same tile of G stripes on neighbouring blocks
+    const u32 G = a.order == 3 ? 2u : 8u;
+    const u32 per = G * a.tps, g = t / per, r = t - g * per;
+    const u32 bt = a.ntiles / a.tps, gsz = bt - g * G < G ? bt - g * G : G;
+    tile = r / gsz; stripe = g * G + (r - tile * gsz);
     return;
   }
   stripe = t / a.tps;
   const u32 r = t - stripe * a.tps;
-  if (a.order == 1) {  // Q8: the same position of 8 column segments of the stripe
-    const u32 seg = a.tps / 8u;
-    tile = r < seg * 8u ? (r % 8u) * seg + r / 8u : r;
+  if (a.order == 1 || a.order == 6) {  // Q8 / Q16: the same position of Q column segments
+    const u32 Q = a.order == 1 ? 8u : 16u, seg = a.tps / Q;
+    tile = r < seg * Q ? (r % Q) * seg + r / Q : r;
   } else {
     tile = r;
   }

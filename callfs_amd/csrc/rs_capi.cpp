@@ -1611,6 +1611,15 @@ int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
     (void)hipFree(plan->dmeta);
     return RS_E_HIP;
   }
+  // plans are launched many times: the launch groups the rule gives the bit-sliced kernel have
+  // it compiled (or loaded from the code cache) here, so every launch runs it; a compile that
+  // fails leaves them on the nibble-table kernels
+  for (size_t gi = 0; gi < t->groups.size(); ++gi) {
+    const Group& g = t->groups[gi];
+    if (g.bsk && bitslice_wanted(group_args(*t, plan->layout, gi, batch,
+                                            static_cast<uint8_t*>(plan->dmeta), S, 1, plan->hint)))
+      (void)g.bsk->function(device, /*wait=*/true);
+  }
   *out = plan.release();
   return RS_OK;
 }
@@ -1817,6 +1826,24 @@ int rs_plan_set_orders(rs_plan* plan, const int* orders, int n) {
   std::lock_guard<std::mutex> g(plan->mu);
   plan->orders = next;
   return RS_OK;
+}
+
+int rs_plan_forms(const rs_plan* plan, int* forms, int max_groups) {
+  if (!plan || max_groups < 0 || (max_groups > 0 && !forms)) return RS_E_ARG;
+  auto* p = const_cast<rs_plan*>(plan);
+  std::vector<int> orders;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    orders = p->orders;
+  }
+  const Tables& t = *plan->tables;
+  auto* d = static_cast<uint8_t*>(plan->dmeta);
+  const int ng = static_cast<int>(t.groups.size());
+  for (int gi = 0; gi < ng && gi < max_groups; ++gi) {
+    const int order = static_cast<size_t>(gi) < orders.size() ? orders[gi] : -1;
+    forms[gi] = launch_form(group_args(t, plan->layout, gi, plan->batch, d, plan->S, 1, plan->hint), order);
+  }
+  return ng;
 }
 
 int rs_plan_stripe_status(rs_plan* plan, void* stream, int* flags) {

@@ -637,12 +637,16 @@ bool can_bitslice(const ApplyArgs& a) {
 }
 // The rule's bit-sliced launches and their order (tile_order.hpp bitslice_rule)
 bool takes_bitslice(const ApplyArgs& a) {
+  const uint32_t rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
   return can_bitslice(a) &&
-         bitslice_rule(a.K, a.R, (a.S / 16 + bs::kTileVecs - 1) / bs::kTileVecs,
-                       (a.in_misalign | a.out_misalign) != 0);
+         bitslice_rule(a.K, a.R, (a.S / 16 + bs::kTileVecs - 1) / bs::kTileVecs, a.in_misalign != 0,
+                       a.out_misalign != 0, (a.verify_mask & rows) != 0,
+                       (a.verify_mask & rows) == rows);
 }
 TileOrder bitslice_rule_order(const ApplyArgs& a) {
-  return bitslice_tile_order((a.S / 16 + bs::kTileVecs - 1) / bs::kTileVecs);
+  const uint32_t rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
+  return bitslice_tile_order((a.S / 16 + bs::kTileVecs - 1) / bs::kTileVecs,
+                             (a.in_misalign | a.out_misalign) != 0, (a.verify_mask & rows) != 0);
 }
 // bs::Args::order of a TileOrder (-1: no generated form)
 int bitslice_order(TileOrder o) {
@@ -651,23 +655,43 @@ int bitslice_order(TileOrder o) {
     case TileOrder::kSeg8: return 1;
     case TileOrder::kXcd32: return 2;
     case TileOrder::kGroup2: return 3;
-    default: return -1;
+    case TileOrder::kXcd8: return 4;
+    case TileOrder::kGroup8: return 5;
+    case TileOrder::kSeg16: return 6;
   }
 }
 }  // namespace
 
+bool bitslice_wanted(const ApplyArgs& a) { return takes_bitslice(a); }
+
+int launch_form(const ApplyArgs& a, int order) {
+  if (order >= 0) return order;
+  if (takes_bitslice(a) && static_cast<const bs::Kernel*>(a.bs)->state() == bs::Kernel::State::kReady)
+    return kOrderBitslice + static_cast<int>(bitslice_rule_order(a));
+  const std::vector<int> c = nibble_candidates(a, false);
+  return c.empty() ? -1 : c[0];
+}
+
 std::vector<int> order_candidates(const ApplyArgs& a, bool every_instance) {
   std::vector<int> c = nibble_candidates(a, every_instance);
+  // the rule's kernel first (rs_plan_tune's bar favours cand[0])
+  if (!c.empty() && takes_bitslice(a)) c.insert(c.begin(), kOrderBitslice + static_cast<int>(bitslice_rule_order(a)));
   if (!c.empty() && can_bitslice(a)) {
     const uint64_t tps = (a.S / 16 + bs::kTileVecs - 1) / bs::kTileVecs;
     auto add = [&c](TileOrder o) {
       const int v = kOrderBitslice + static_cast<int>(o);
       if (std::find(c.begin(), c.end(), v) == c.end()) c.push_back(v);
     };
+    add(bitslice_rule_order(a));
     add(TileOrder::kConsecutive);
-    add(TileOrder::kXcd32);
-    if (tps <= 64 || every_instance) add(TileOrder::kGroup2);
+    add(TileOrder::kGroup2);
+    if (tps <= 32 || every_instance) add(TileOrder::kGroup8);
     if (tps >= 64 || every_instance) add(TileOrder::kSeg8);
+    if (tps > 1024 || every_instance) add(TileOrder::kSeg16);
+    if (every_instance) {
+      add(TileOrder::kXcd8);
+      add(TileOrder::kXcd32);
+    }
   }
   return c;
 }

@@ -140,10 +140,11 @@ constexpr int kOrderDma = 192;
 // (kOrderTriDbG + 0 / 1: R <= 4, K >= 6 double-buffered triples with the tiles of 4 / 8 stripes
 // interleaved (G4 / G8); A/B build)
 constexpr int kOrderTriDbG = 224;
-// (kOrderBitslice + consecutive / G2 / Q8 / X32: the launch group's bit-sliced kernel,
-// ApplyArgs::bs; R >= kBitsliceMinRows)
+// (kOrderBitslice + any TileOrder: the launch group's bit-sliced kernel, ApplyArgs::bs,
+// DESIGN.md §5.7; every launch group gets one: the rule takes it for wide groups and
+// rs_plan_tune times it for every group)
 constexpr int kOrderBitslice = 256;
-constexpr int kBitsliceMinRows = 5;
+constexpr int kBitsliceMinRows = 1;
 
 // `order` >= 0 (a TileOrder) replaces the measured rule for this launch where the
 // chosen kernel has an instance in that order (order_candidates lists them); -1 = the
@@ -163,6 +164,14 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only = false
 // no choice (byte kernel, realigning kernel, S < 16). every_instance: also the orders
 // that have an instance but never measured faster (rs_plan_set_orders accepts them).
 std::vector<int> order_candidates(const ApplyArgs& a, bool every_instance = false);
+
+// True when the rule runs launch `a` on its bit-sliced kernel (ApplyArgs::bs) once that is
+// compiled (rs_plan_create compiles it up front for such launches).
+bool bitslice_wanted(const ApplyArgs& a);
+
+// The form (an order code as order_candidates lists them) launch_apply runs for `order`
+// (-1 = the rule, whose bit-sliced choice counts once its kernel is compiled).
+int launch_form(const ApplyArgs& a, int order);
 
 // Measurement only (rs_plan_launch_ceiling), for launch `a` in the order the production
 // launch takes (`order` as for launch_apply), on the production grid and slicing:

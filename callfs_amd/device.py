@@ -222,8 +222,8 @@ class Plan:
                    100: "tri-q16", 101: "tri-x8", 102: "tri-x32", 128: "realign-tri", 133: "realign-tri-x8",
                    134: "realign-tri-x32", 160: "realign64", 165: "realign64-x8",
                    166: "realign64-x32", 192: "dma", 194: "dma-g2", 195: "dma-q8",
-                   198: "dma-x32", 224: "tridb-g4", 225: "tridb-g8", 256: "bs", 258: "bs-g2",
-                   259: "bs-q8", 262: "bs-x32"}
+                   198: "dma-x32", 224: "tridb-g4", 225: "tridb-g8", 256: "bs", 257: "bs-g8",
+                   258: "bs-g2", 259: "bs-q8", 260: "bs-q16", 261: "bs-x8", 262: "bs-x32"}
 
     def tune(self, reps: int = 5, stream: Optional[torch.cuda.Stream] = None) -> list:
         """rs_plan_tune: time each launch group in every tile order its kernel offers
@@ -243,6 +243,17 @@ class Plan:
         codes = {v: k for k, v in self.ORDER_NAMES.items()}
         arr = (ctypes.c_int * len(names))(*[codes[nm] for nm in names])
         N.check(N.lib.rs_plan_set_orders(self.handle, arr, len(names)), "rs_plan_set_orders")
+
+    def forms(self) -> list:
+        """rs_plan_forms: the kernel form (order name) each launch group of the next launch
+        runs: the pinned or tuned order, else the rule's ("bs-*" once the rule's bit-sliced
+        kernel is compiled)."""
+        n = int(N.lib.rs_plan_groups(self.handle))
+        out = (ctypes.c_int * max(n, 1))()
+        got = N.lib.rs_plan_forms(self.handle, out, n)
+        if got < 0:
+            N.check(got, "rs_plan_forms")
+        return [self.ORDER_NAMES.get(out[i], str(out[i])) for i in range(n)]
 
     def corrupt(self, stream: Optional[torch.cuda.Stream] = None) -> bool:
         """Synchronises the stream; True when a Verify row mismatched (then clears)."""

@@ -194,12 +194,21 @@ void rs_plan_destroy(rs_plan* plan);
  * XCD8 or XCD32); on such launches RS_ORDER_0..6 name the plain kernel with unaligned
  * 16-B accesses in that tile order */
 #define RS_ORDER_REALIGN 32
+/* the launch group's bit-sliced kernel: an XOR network over bit planes
+ * generated for the group's coefficient block and compiled at plan time (hiprtc; cached on
+ * disk), RS_ORDER_BITSLICE + the tile order it runs in (RS_ORDER_0..6) */
+#define RS_ORDER_BITSLICE 256
 int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups);
 /* Sets the tile order of launch groups 0..n-1 (the others: the rule) to orders[i], as
  * rs_plan_tune would: RS_ORDER_* that the group's kernel has an instance of (what
  * rs_plan_tune times, and XCD8 / XCD32 on aligned shards), or -1 for the rule. RS_E_ARG if any entry is not offered or n
  * exceeds rs_plan_groups; the plan is then unchanged. For orders tuned once and kept. */
 int  rs_plan_set_orders(rs_plan* plan, const int* orders, int n);
+/* The kernel form each launch group of the next rs_plan_launch runs, up to max_groups
+ * entries: the pinned or tuned order, else the rule's (RS_ORDER_BITSLICE + its tile order
+ * where the rule gives the group the bit-sliced kernel; the codes rs_plan_tune reports).
+ * Returns the number of launch groups, or RS_E_ARG. */
+int  rs_plan_forms(const rs_plan* plan, int* forms, int max_groups);
 /* Measurement only (no upstream counterpart): enqueues the plan's launch groups as a
  * traffic ceiling of the same shape, on the production grid, tile order and slicing, for
  * a roofline denominator measured in the same process (bench.py):

@@ -11,6 +11,10 @@
 //     round-robin device slots, split ways and column part boundaries
 //  7. per-device kernel setup (DeviceOnce): the wide kernels' dynamic-LDS opt-in is issued
 //     once per (device, R), before the first such launch on each device
+//  8. the bit-sliced kernels' generator (bitslice_gen.hpp): the bit transpose against its
+//     definition, each coefficient's GF(2) matrix against the field, the XOR network of
+//     random coefficient blocks (zeros included) against a scalar GF multiply, the rule
+//     and order bounds, and that the generated source declares every accumulator
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -19,6 +23,7 @@
 #include <thread>
 #include <vector>
 
+#include "bitslice_gen.hpp"
 #include "copy_pool.hpp"
 #include "dispatch.hpp"
 #include "gf256.hpp"
@@ -497,6 +502,89 @@ int main() {
     once2.run(0, 70, [&] { n++; });
     CHECK(n == 3);
   }
+  // 8. bit-sliced kernels (bitslice_gen.hpp)
+  {
+    std::mt19937 rng(0xB175);
+    // tr8: bit i of byte p of out[k] == bit k of byte p of in[i]; an involution
+    for (int t = 0; t < 64; ++t) {
+      uint32_t in[8], d[8];
+      for (int i = 0; i < 8; ++i) in[i] = d[i] = rng();
+      bs::tr8(d);
+      bool ok = true;
+      for (int k = 0; k < 8; ++k)
+        for (int i = 0; i < 8; ++i)
+          for (int p = 0; p < 4; ++p)
+            ok &= ((d[k] >> (8 * p + i)) & 1u) == ((in[i] >> (8 * p + k)) & 1u);
+      CHECK(ok);
+      bs::tr8(d);
+      CHECK(std::equal(d, d + 8, in));
+    }
+    // M_c: c*x == XOR over set bits j of x of column j, for every (c, x)
+    {
+      const GF& g = gf();
+      bool ok = true;
+      for (int c = 0; c < 256; ++c) {
+        uint8_t rows[8];
+        bs::mul_matrix(static_cast<uint8_t>(c), rows);
+        for (int x = 0; x < 256; ++x) {
+          uint8_t y = 0;
+          for (int k = 0; k < 8; ++k)
+            y |= static_cast<uint8_t>((__builtin_popcount(rows[k] & x) & 1) << k);
+          ok &= y == g.mul[c][x];
+        }
+      }
+      CHECK(ok);
+    }
+    // the network: random blocks (a third of the coefficients zero), 32 random bytes per
+    // input and lane, against the scalar multiply byte by byte
+    const GF& g = gf();
+    for (int t = 0; t < 40; ++t) {
+      const int K = 1 + static_cast<int>(rng() % 40), R = 1 + static_cast<int>(rng() % 16);
+      std::vector<uint8_t> coef(static_cast<size_t>(K) * R);
+      for (auto& c : coef) c = rng() % 3 == 0 ? 0 : static_cast<uint8_t>(rng());
+      const bs::Network net = bs::build_network(K, R, coef.data());
+      std::vector<std::array<uint32_t, 8>> in(K), out;
+      for (auto& v : in)
+        for (auto& w : v) w = rng();
+      bs::evaluate(net, in, out);
+      bool ok = static_cast<int>(out.size()) == R;
+      for (int r = 0; r < R && ok; ++r)
+        for (int w = 0; w < 8; ++w)
+          for (int p = 0; p < 4; ++p) {
+            uint8_t want = 0;
+            for (int i = 0; i < K; ++i)
+              want ^= g.mul[coef[static_cast<size_t>(r) * K + i]][(in[i][w] >> (8 * p)) & 0xffu];
+            ok &= ((out[r][w] >> (8 * p)) & 0xffu) == want;
+          }
+      CHECK(ok);
+      // the generated kernel: every used accumulator declared, one pin per shard group
+      const std::string src = bs::kernel_source(net, "rs_bs", bs::GenOptions{}, 56);
+      CHECK(src.find("void rs_bs(const Args a)") != std::string::npos);
+      CHECK(src.find("static_assert(sizeof(Args) == 56") != std::string::npos);
+      for (int r = 0; r < R; ++r) {
+        char nm[32];
+        std::snprintf(nm, sizeof nm, " a%d_7", r);
+        CHECK(src.find(nm) != std::string::npos);
+      }
+    }
+    // the rule: every wide group; R 5..8 for many inputs or misaligned one-shard decodes;
+    // never R <= 4 or read-only launches; orders by tiles per stripe
+    CHECK(bitslice_rule(10, 9, 128, false, false, false, false));
+    CHECK(bitslice_rule(2, 16, 1, true, true, true, true));
+    CHECK(bitslice_rule(32, 8, 256, false, false, false, false));
+    CHECK(!bitslice_rule(10, 8, 128, false, false, false, false));
+    CHECK(bitslice_rule(10, 8, 68, true, false, true, false));
+    CHECK(!bitslice_rule(10, 8, 68, true, true, true, false));
+    CHECK(!bitslice_rule(10, 8, 68, true, false, true, true));
+    CHECK(!bitslice_rule(32, 4, 128, false, false, false, false));
+    CHECK(bitslice_rule(16, 8, 128, false, false, false, false));
+    CHECK(!bitslice_rule(16, 8, 32, false, false, false, false));
+    CHECK(bitslice_tile_order(8, false, false) == TileOrder::kGroup8);
+    CHECK(bitslice_tile_order(128, false, false) == TileOrder::kGroup2);
+    CHECK(bitslice_tile_order(512, false, false) == TileOrder::kSeg8);
+    CHECK(bitslice_tile_order(512, true, true) == TileOrder::kXcd32);
+  }
+
   std::printf(fails ? "FAILED %d\n" : "host_test ok\n", fails);
   return fails ? 1 : 0;
 }

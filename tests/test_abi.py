@@ -92,6 +92,7 @@ def test_plan_entry_points_refuse_null_plans(native_lib):
     assert L.rs_plan_launch_ceiling_timed(None, None, 1, None, None) == E
     assert L.rs_plan_tune(None, None, 1, None, 0) == E
     assert L.rs_plan_groups(None) == 0
+    assert L.rs_plan_forms(None, orders, 2) == E
 
 
 def test_init_fails_loudly_without_gpu(native_lib):

@@ -1253,6 +1253,8 @@ def test_plan_tune_then_launch_bit_exact(native_lib, k, m, S, batch, erase):
     assert len(names) == max(1, -(-m // 16))
     plain = {"consecutive", "g8", "g2", "q8", "q16", "x8", "x32"}
     tri = {"tri", "tri-g2", "tri-x32", "tri-q8", "tri-q16", "tri-x8"}
+    # every group may also take its bit-sliced kernel, in any tile order
+    plain |= {"bs", "bs-g8", "bs-g2", "bs-q8", "bs-q16", "bs-x8", "bs-x32"}
     # a launch group with R <= 8 rows may also take the triple loads: up to 16 inputs, or
     # any count at R <= 4 (the double-buffered form); groups of 9..16 rows never do
     for gi, name in enumerate(names):
@@ -1290,7 +1292,8 @@ ALL_ORDER_NAMES = ["consecutive", "g8", "g2", "q8", "q16", "x8", "x32", "realign
                    "realign-x8", "realign-x32", "wix", "wix-g8", "wix-g2", "wix-q8", "wix-q16",
                    "wix-x8", "wix-x32", "tri", "tri-g2", "tri-x32", "tri-q8", "tri-q16",
                    "tri-x8", "realign-tri", "realign-tri-x8", "realign-tri-x32",
-                   "dma", "dma-g2", "dma-q8", "dma-x32", "tridb-g4", "tridb-g8"]
+                   "dma", "dma-g2", "dma-q8", "dma-x32", "tridb-g4", "tridb-g8",
+                   "bs", "bs-g8", "bs-g2", "bs-q8", "bs-q16", "bs-x8", "bs-x32"]
 
 
 @pytest.mark.parametrize("k,m,S,batch,off,erase", [

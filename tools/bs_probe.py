@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--layout", default="planar")
+    ap.add_argument("--fresh", type=int, default=0,
+                    help="1: decodes rebuild the erased shards into fresh buffers")
+    ap.add_argument("--tune", type=int, default=0, help="1: also an rs_plan_tune plan")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
@@ -67,16 +70,35 @@ def main():
         if erase != "-":
             lost = sorted({int(x) for x in erase.split("+")})
             present = [i not in lost for i in range(n)]
+        fresh = None
+        if a.fresh and present is not None:
+            # the erased shards rebuilt into buffers of their own (64-B pitch, 256-B aligned),
+            # as upstream Reconstruct allocates missing shards (bench.py --decode-into fresh)
+            from callfs_amd.device import _aligned_empty
+            fp = -(-S // 64) * 64
+            fresh = _aligned_empty((B, len(lost), fp), 256, dev)
+            ptrs = list(ptrs)
+            for b in range(B):
+                for j, i in enumerate(lost):
+                    ptrs[b * n + i] = fresh[b, j].data_ptr()
         rule = Plan(k, m, S, B, ptrs, present=present)
         plans = {"rule": rule}
-        out = {"shape": spec, "k": k, "m": m, "S": S, "stripes": B, "erase": erase}
+        out = {"shape": spec, "k": k, "m": m, "S": S, "stripes": B, "erase": erase,
+               "layout": a.layout, "fresh": fresh is not None}
 
         def exact(p):
-            for i in lost:
-                sb.zero_shard(i)
+            if fresh is not None:
+                fresh.zero_()
+            else:
+                for i in lost:
+                    sb.zero_shard(i)
             p.launch(stream)
             torch.cuda.synchronize()
-            return bool(torch.equal(sb.gather(), ref)) and not p.corrupt(stream)
+            if fresh is not None:
+                ok = all(torch.equal(fresh[:, j, :S], ref[:, i]) for j, i in enumerate(lost))
+            else:
+                ok = bool(torch.equal(sb.gather(), ref))
+            return ok and not p.corrupt(stream)
 
         out["bit_exact"] = {"rule": exact(rule)}
         for o in a.orders.split(","):
@@ -92,6 +114,11 @@ def main():
             out.setdefault("first_launch_s", {})[o] = round(time.perf_counter() - t0, 2)
             out["bit_exact"][o] = exact(p)
             plans[o] = p
+        if a.tune:
+            tp = Plan(k, m, S, B, ptrs, present=present)
+            out["tuned_orders"] = tp.tune(stream=stream)
+            out["bit_exact"]["tuned"] = exact(tp)
+            plans["tuned"] = tp
         t = {v: [] for v in plans}
         for r in range(a.rounds):
             names = list(plans)
@@ -101,7 +128,7 @@ def main():
         nb = rule.bytes
         out["pct_of_8TBs"] = {v: round(nb / (min(x) * 1e-3) / 1e9 / PEAK * 100, 2) for v, x in t.items()}
         print(json.dumps(out), flush=True)
-        del plans, rule, sb, ref
+        del plans, rule, sb, ref, fresh
         torch.cuda.empty_cache()
 
 
