@@ -149,9 +149,16 @@ Mode mode() {
 }
 
 Kernel::Kernel(int K, int R, const uint8_t* coef) : net_(build_network(K, R, coef)) {
+  (void)R;
+  opt_.prefetch = 0;   // auto at compile time (compile_locked)
+  opt_.min_waves = 0;  // auto_waves at compile time
   // development knobs (tools/bs_probe.py): prefetch depth and the waves-per-SIMD floor
   if (const char* e = std::getenv("CALLFS_RS_BS_PREFETCH")) opt_.prefetch = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CALLFS_RS_BS_WAVES")) opt_.min_waves = std::max(1, std::min(8, std::atoi(e)));
+  if (const char* e = std::getenv("CALLFS_RS_BS_BLOCK")) {
+    const int b = std::atoi(e);
+    if (b == 64 || b == 128 || b == 256 || b == 512 || b == 1024) opt_.block = b;
+  }
 }
 
 Kernel::~Kernel() {
@@ -186,18 +193,69 @@ bool Kernel::compile_now() {
   }
 }
 
+namespace {
+// One hiprtc compile of `src`; the code object, or empty with *err set. *spills = the
+// compiler's "VGPRs Spill" remark for the kernel (-1 when the log has none).
+std::vector<char> rtc_compile(const std::string& src, const std::vector<std::string>& opts,
+                              std::string* err, int* spills) {
+  std::vector<char> code;
+  *spills = -1;
+  hiprtcProgram p = nullptr;
+  if (hiprtcCreateProgram(&p, src.c_str(), "rs_bs.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    *err = "hiprtcCreateProgram failed";
+    return code;
+  }
+  std::vector<const char*> o;
+  for (const auto& x : opts) o.push_back(x.c_str());
+  const hiprtcResult r = hiprtcCompileProgram(p, static_cast<int>(o.size()), o.data());
+  size_t n = 0;
+  (void)hiprtcGetProgramLogSize(p, &n);
+  std::string log(n, '\0');
+  if (n) (void)hiprtcGetProgramLog(p, &log[0]);
+  const size_t at = log.find("VGPRs Spill:");
+  if (at != std::string::npos) *spills = std::atoi(log.c_str() + at + 12);
+  if (r != HIPRTC_SUCCESS) {
+    *err = std::string("hiprtc: ") + hiprtcGetErrorString(r) + "\n" + log;
+  } else {
+    if (hiprtcGetCodeSize(p, &n) == HIPRTC_SUCCESS && n) {
+      code.resize(n);
+      if (hiprtcGetCode(p, code.data()) != HIPRTC_SUCCESS) code.clear();
+    }
+    if (code.empty()) *err = "hiprtc: no code object";
+  }
+  (void)hiprtcDestroyProgram(&p);
+  return code;
+}
+
+// Waves per SIMD to ask for: the VGPRs a group needs are about 8 accumulator planes per row,
+// 8 per input shard in flight and ~40 for the planes and combos of the shard being consumed
+// and addresses; 512 VGPRs per SIMD lane (tools/bs_params_r06.sh, profiles/r06/params1: R = 8
+// at 4 waves 75.9 -> 79.1 % for RS(32,8) 2 MiB; R = 16 forced to 3 waves spilled ~1,000 VGPRs
+// and ran at 12 %).
+int auto_waves(int R, int prefetch) {
+  const int need = 8 * R + 8 * (prefetch + 1) + 40;
+  return std::max(1, std::min(8, 512 / need));
+}
+constexpr int kSpillLimit = 16;  // VGPRs spilled that a floor may cost before it is lowered
+}  // namespace
+
 void Kernel::compile_locked(std::unique_lock<std::mutex>& lk) {
   state_ = State::kCompiling;
   const Network net = net_;
-  const GenOptions opt = opt_;
+  GenOptions opt = opt_;
   lk.unlock();
   const auto t0 = std::chrono::steady_clock::now();
   const std::string arch = target_arch();
-  const std::string src = kernel_source(net, "rs_bs", opt, sizeof(Args));
+  // two shards in flight; groups that run at 2 waves per SIMD anyway have the registers for
+  // four (profiles/r06/params1: RS(32,16) 74.8 -> 75.3 %, RS(20,16) 256 KiB 74.8 -> 75.3 %)
+  if (opt.prefetch <= 0) opt.prefetch = auto_waves(net.R, 2) <= 2 ? 4 : 2;
+  if (opt.min_waves <= 0) opt.min_waves = auto_waves(net.R, opt.prefetch);
+  std::string src = kernel_source(net, "rs_bs", opt, sizeof(Args));
   int ver_major = 0, ver_minor = 0;
   (void)hiprtcVersion(&ver_major, &ver_minor);
   const std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17",
-                                         "-fno-gpu-rdc"};
+                                         "-fno-gpu-rdc", "-Rpass-analysis=kernel-resource-usage"};
+  // keyed by the first source tried: the cache holds the code object the search accepted
   std::string keytxt = src + arch + std::to_string(ver_major) + "." + std::to_string(ver_minor);
   for (const auto& o : opts) keytxt += o;
   char name[64];
@@ -206,30 +264,15 @@ void Kernel::compile_locked(std::unique_lock<std::mutex>& lk) {
   const std::string path = dir.empty() ? std::string() : dir + "/" + name;
   std::vector<char> code;
   std::string err;
+  int spills = -1;
   if (path.empty() || !read_file(path, code)) {
     code.clear();
-    hiprtcProgram p = nullptr;
-    if (hiprtcCreateProgram(&p, src.c_str(), "rs_bs.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
-      err = "hiprtcCreateProgram failed";
-    } else {
-      std::vector<const char*> o;
-      for (const auto& s : opts) o.push_back(s.c_str());
-      const hiprtcResult r = hiprtcCompileProgram(p, static_cast<int>(o.size()), o.data());
-      if (r != HIPRTC_SUCCESS) {
-        size_t n = 0;
-        (void)hiprtcGetProgramLogSize(p, &n);
-        std::string log(n, '\0');
-        if (n) (void)hiprtcGetProgramLog(p, &log[0]);
-        err = std::string("hiprtc: ") + hiprtcGetErrorString(r) + "\n" + log;
-      } else {
-        size_t n = 0;
-        if (hiprtcGetCodeSize(p, &n) == HIPRTC_SUCCESS && n) {
-          code.resize(n);
-          if (hiprtcGetCode(p, code.data()) != HIPRTC_SUCCESS) code.clear();
-        }
-        if (code.empty()) err = "hiprtc: no code object";
-      }
-      (void)hiprtcDestroyProgram(&p);
+    // lower the waves-per-SIMD floor while the compiler spills more than kSpillLimit VGPRs
+    for (;;) {
+      code = rtc_compile(src, opts, &err, &spills);
+      if (code.empty() || spills <= kSpillLimit || opt.min_waves <= 1) break;
+      --opt.min_waves;
+      src = kernel_source(net, "rs_bs", opt, sizeof(Args));
     }
     if (!code.empty() && !path.empty()) write_file(dir, path, code);
   }
@@ -237,6 +280,8 @@ void Kernel::compile_locked(std::unique_lock<std::mutex>& lk) {
       std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   lk.lock();
   compile_s_ = secs;
+  spills_ = spills;
+  waves_ = opt.min_waves;
   if (code.empty()) {
     error_ = err;
     state_ = State::kFailed;
@@ -246,8 +291,8 @@ void Kernel::compile_locked(std::unique_lock<std::mutex>& lk) {
     code_ = std::move(code);
     state_ = State::kReady;
     if (std::getenv("CALLFS_RS_BITSLICE_LOG"))
-      std::fprintf(stderr, "callfs_rs bitslice K=%d R=%d: %zu B code object in %.2f s\n", net.K,
-                   net.R, code_.size(), secs);
+      std::fprintf(stderr, "callfs_rs bitslice K=%d R=%d: %zu B code object, %d waves floor, "
+                   "%d VGPRs spilled, %.2f s\n", net.K, net.R, code_.size(), waves_, spills, secs);
   }
   cv_.notify_all();
 }
@@ -302,17 +347,18 @@ std::shared_ptr<Kernel> kernel_for(int K, int R, const uint8_t* coef) {
   return k;
 }
 
-hipError_t launch(hipFunction_t fn, const Args& a, uint32_t tiles, hipStream_t stream,
+hipError_t launch(hipFunction_t fn, const Args& a, uint32_t tiles, int block, hipStream_t stream,
                   hipEvent_t ev_start, hipEvent_t ev_stop) {
   Args args = a;
   size_t size = sizeof args;
   void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                     HIP_LAUNCH_PARAM_END};
   if (ev_start || ev_stop)
-    return hipExtModuleLaunchKernel(fn, tiles * static_cast<uint32_t>(kBlockThreads), 1, 1,
-                                    kBlockThreads, 1, 1, 0, stream, nullptr, config, ev_start,
-                                    ev_stop, 0);
-  return hipModuleLaunchKernel(fn, tiles, 1, 1, kBlockThreads, 1, 1, 0, stream, nullptr, config);
+    return hipExtModuleLaunchKernel(fn, tiles * static_cast<uint32_t>(block), 1, 1,
+                                    static_cast<uint32_t>(block), 1, 1, 0, stream, nullptr, config,
+                                    ev_start, ev_stop, 0);
+  return hipModuleLaunchKernel(fn, tiles, 1, 1, static_cast<uint32_t>(block), 1, 1, 0, stream,
+                               nullptr, config);
 }
 
 }  // namespace bs

@@ -29,6 +29,8 @@ class Kernel : public std::enable_shared_from_this<Kernel> {
 
   int K() const { return net_.K; }
   int R() const { return net_.R; }
+  int block_threads() const { return opt_.block; }
+  int tile_vecs() const { return opt_.tile_vecs(); }
   State state() const;
   // Queues the compile on the background worker (no-op once queued or done).
   void compile_async();
@@ -40,6 +42,8 @@ class Kernel : public std::enable_shared_from_this<Kernel> {
   hipFunction_t function(int device, bool wait);
   // Compiler-reported resources of the code object (0 before it exists).
   int vgprs() const { return vgprs_; }
+  int waves_floor() const { return waves_; }
+  int spills() const { return spills_; }
   double compile_seconds() const { return compile_s_; }
   const std::string& error() const { return error_; }
 
@@ -55,6 +59,8 @@ class Kernel : public std::enable_shared_from_this<Kernel> {
   std::vector<char> code_;
   std::string error_;
   int vgprs_ = 0;
+  int waves_ = 0;
+  int spills_ = -1;
   double compile_s_ = 0;
   hipModule_t mod_[kMaxDevices] = {};
   hipFunction_t fn_[kMaxDevices] = {};
@@ -68,9 +74,9 @@ std::shared_ptr<Kernel> kernel_for(int K, int R, const uint8_t* coef);
 enum class Mode { kOff, kAuto, kSync };
 Mode mode();
 
-// Launches rs_bs over `tiles` tiles starting at a.t_base (kBlockThreads threads per tile);
+// Launches rs_bs over `tiles` tiles starting at a.t_base (`block` threads per tile);
 // ev_start / ev_stop as hipExtModuleLaunchKernel takes them.
-hipError_t launch(hipFunction_t fn, const Args& a, uint32_t tiles, hipStream_t stream,
+hipError_t launch(hipFunction_t fn, const Args& a, uint32_t tiles, int block, hipStream_t stream,
                   hipEvent_t ev_start, hipEvent_t ev_stop);
 
 }  // namespace bs

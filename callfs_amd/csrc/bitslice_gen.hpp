@@ -37,7 +37,7 @@ constexpr int kMaxRows = 16;
 constexpr int kMaxInputs = 256;
 // 16-B vectors per wave-tile: lane l owns vectors base + l and base + 64 + l
 constexpr int kWaveVecs = 128;
-constexpr int kBlockThreads = 256;
+constexpr int kBlockThreads = 256;  // default block (GenOptions::block)
 constexpr int kTileVecs = kWaveVecs * (kBlockThreads / 64);  // 512 vectors = 8 KiB per shard
 
 // Kernel arguments. The generated source declares the same struct (kArgsDecl); bitslice.cpp
@@ -168,7 +168,9 @@ inline void evaluate(const Network& n, const std::vector<std::array<uint32_t, 8>
 
 struct GenOptions {
   int prefetch = 2;  // input shards whose loads are in flight while one is computed
-  int min_waves = 2; // amdgpu_waves_per_eu lower bound
+  int min_waves = 2; // amdgpu_waves_per_eu lower bound (bitslice.cpp: 0 = auto_waves)
+  int block = kBlockThreads;  // threads per block: a tile is block / 64 * kWaveVecs vectors
+  int tile_vecs() const { return block / 64 * kWaveVecs; }
 };
 
 namespace detail {
@@ -282,12 +284,12 @@ __device__ __forceinline__ void map_tile(const Args& a, u32 b, u32& stripe, u32&
 }
 )SRC";
   o += fmt("extern \"C\" __global__ __launch_bounds__(%d) __attribute__((amdgpu_waves_per_eu(%d, 8)))\n",
-           kBlockThreads, opt.min_waves);
+           opt.block, opt.min_waves);
   o += fmt("void %s(const Args a) {\n", name.c_str());
   o += "  u32 stripe, tile;\n  map_tile(a, blockIdx.x, stripe, tile);\n";
   o += "  if (stripe * a.tps + tile >= a.ntiles) return;\n";
   o += fmt("  const u64 va = (u64)tile * %d + (threadIdx.x >> 6) * %d + (threadIdx.x & 63u);\n",
-           kTileVecs, kWaveVecs);
+           opt.tile_vecs(), kWaveVecs);
   o += "  if (va >= a.nvec) return;\n  const bool lb = va + 64 < a.nvec;\n";
   o += fmt("  const cptr<const unsigned char*> in = (cptr<const unsigned char*>)(a.in_tab) + (u64)stripe * %d;\n", n.K);
   o += fmt("  const cptr<unsigned char*> out = (cptr<unsigned char*>)(a.out_tab) + (u64)stripe * %d;\n", n.R);

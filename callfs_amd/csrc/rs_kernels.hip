@@ -831,7 +831,7 @@ bool launch_bitslice(ApplyArgs a, hipStream_t stream, TileOrder ord, LaunchEvent
   b.out_tab = a.out_tab;
   b.status = a.status;
   b.nvec = a.S / 16;
-  b.tps = static_cast<uint32_t>((b.nvec + bs::kTileVecs - 1) / bs::kTileVecs);
+  b.tps = static_cast<uint32_t>((b.nvec + k->tile_vecs() - 1) / k->tile_vecs());
   b.ntiles = b.tps * static_cast<uint32_t>(a.batch);
   b.verify_mask = a.verify_mask;
   b.status_stride = a.status_stride;
@@ -839,8 +839,8 @@ bool launch_bitslice(ApplyArgs a, hipStream_t stream, TileOrder ord, LaunchEvent
   const bool tail_after = b.nvec * 16 < a.S;
   launch_sliced(b.ntiles, a.K + a.R, a, [&](uint32_t blocks, bool first, bool last) {
     b.t_base = a.t_base;
-    const hipError_t e = bs::launch(fn, b, blocks, stream, first ? ev.start : nullptr,
-                                    last && !tail_after ? ev.stop : nullptr);
+    const hipError_t e = bs::launch(fn, b, blocks, k->block_threads(), stream,
+                                    first ? ev.start : nullptr, last && !tail_after ? ev.stop : nullptr);
     if (e != hipSuccess && *err == hipSuccess) *err = e;
   });
   if (*err != hipSuccess) return true;

@@ -82,12 +82,15 @@ constexpr int kTileOrders = 7;
 //  * R 5..8 with compared rows on misaligned inputs (one-shard decodes of the io.ReadAll
 //    layout, rebuilt into fresh buffers): RS(10,8) 553,574 B {1} 65.1 -> 74.9, 122,190 B 66.2
 //    -> 74.8, RS(8,8) 312,855 B 65.8 -> 74.3 (X32 / G8), RS(16,8) 1 MiB 73.7 -> 77.0;
-//  * R <= 4: the nibble tables run at the HBM ceiling; only K >= 24 at 1 MiB gained (RS(32,4)
-//    72.7 -> 74.7), which rs_plan_tune finds, so the rule leaves R <= 4 alone.
+//  * R <= 4: the nibble tables run at the HBM ceiling, except for K >= 24 inputs at 0.5 - 1 MiB
+//    shards (G2), on two boxes: RS(32,4) 1 MiB 72.7 -> 74.7 / 72.4 -> 74.8, RS(24,4) 74.1 ->
+//    75.5 / 74.0 -> 75.6 (profiles/r06/sweep1, sweep2); RS(20,4) 3.4 MB and RS(16,4) 4 MiB
+//    lose 2-3 points.
 inline bool bitslice_rule(int K, int R, uint64_t tps, bool in_misaligned, bool out_misaligned,
                           bool verify, bool read_only) {
   if (R > 8) return true;
-  if (R <= 4 || read_only) return false;
+  if (read_only) return false;
+  if (R <= 4) return K >= 24 && tps >= 64 && tps <= 128 && !verify && !in_misaligned && !out_misaligned;
   if (verify && in_misaligned && !out_misaligned) return true;
   if (K >= 20) return true;
   return K >= 16 && tps >= 64 && tps <= 256;

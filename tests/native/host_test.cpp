@@ -576,7 +576,10 @@ int main() {
     CHECK(bitslice_rule(10, 8, 68, true, false, true, false));
     CHECK(!bitslice_rule(10, 8, 68, true, true, true, false));
     CHECK(!bitslice_rule(10, 8, 68, true, false, true, true));
-    CHECK(!bitslice_rule(32, 4, 128, false, false, false, false));
+    CHECK(bitslice_rule(32, 4, 128, false, false, false, false));
+    CHECK(!bitslice_rule(32, 4, 256, false, false, false, false));
+    CHECK(!bitslice_rule(16, 4, 128, false, false, false, false));
+    CHECK(!bitslice_rule(10, 4, 128, false, false, false, false));
     CHECK(bitslice_rule(16, 8, 128, false, false, false, false));
     CHECK(!bitslice_rule(16, 8, 32, false, false, false, false));
     CHECK(bitslice_tile_order(8, false, false) == TileOrder::kGroup8);
