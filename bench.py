@@ -454,7 +454,7 @@ def main(argv=None):
         del ref
 
     # untimed: pick each plan's tile order on this box (the outputs are recomputed to the
-    # same bytes; DESIGN.md §5 "Tile order")
+    # same bytes; DESIGN.md §6.2 "Tile order")
     orders = ({"encode": enc.tune(stream=stream), "decode": dec.tune(stream=stream)}
               if args.tune else None)
 
@@ -596,6 +596,7 @@ def main(argv=None):
                 f"{threads} of {visible} visible cores: the GPU box's CPU share per GPU is "
                 f"{CPU_SHARE} (its affinity mask shows the whole host); --cpu-threads "
                 "overrides")
+    wrong = None
     if layout == "planar" and args.layout_ab and world == 1 and not S_obj:
         # (one process only: a second resident batch beside the first; freed buffers first)
         del rebuilt
@@ -604,14 +605,19 @@ def main(argv=None):
             line["layout_ab"] = layout_ab(k, m, S, B, dev, present, stream, args.tune, args.pitch)
             line["layout_ab"]["planar"] = {"encode_frac": line["roofline"]["frac"],
                                            "decode_frac": line["roofline_decode"]["frac"]}
-        except (RuntimeError, SystemExit) as e:  # recorded, never at the cost of the line
+        except RuntimeError as e:  # e.g. an allocation failure: recorded, not at the cost of the line
             line["layout_ab"] = {"error": str(e)[:300]}
+        except SystemExit as e:  # a flagged decode or wrong bytes: printed with the line, then fatal
+            line["layout_ab"] = {"error": str(e)[:300]}
+            wrong = e
     if rank == 0:
         print(json.dumps(line), flush=True)
     enc.close()
     dec.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+    if wrong is not None:
+        raise wrong
 
 
 if __name__ == "__main__":

@@ -11,13 +11,17 @@ import json
 import os
 import subprocess
 import sys
+import threading
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcallfs_rs.so")
 # The A/B build (rs_kernels.hpp CALLFS_RS_AB_INSTANCES): the product plus the measurement-only
-# kernel forms and toggles, for the development tools (CALLFS_RS_LIB=<this path>).
-LIB_AB = os.path.join(HERE, "libcallfs_rs_ab.so")
+# kernel forms and toggles, for the development tools (CALLFS_RS_LIB=<this path>). Built on
+# demand (`python callfs_amd/build.py --ab`, the probe scripts run it on the GPU box) into
+# build/ab/, outside the package: gpurun pushes and the round-end runs carry only the product.
+LIB_AB = os.path.join(os.path.dirname(HERE), "build", "ab", "libcallfs_rs_ab.so")
 # Per-kernel register / scratch / occupancy report of the last build (the compiler's
 # kernel-resource-usage remarks), checked by tests/test_kernel_resources.py: the LDS
 # kernel's speed depends on its waves per SIMD.
@@ -73,9 +77,23 @@ def build(force: bool = False, extra_flags=None, ab: bool = False) -> str:
             cmd.append("-Rpass-analysis=kernel-resource-usage")
         return src, obj, cmd, subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
 
-    # the sources compile independently: in parallel (rs_kernels.hip dominates)
-    with concurrent.futures.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        results = list(ex.map(compile_one, SOURCES))
+    # the sources compile independently: in parallel (rs_kernels.hip dominates). A line on
+    # stderr every 30 s: a GPU-box command that prints nothing for 3 minutes counts as hung
+    done = threading.Event()
+
+    def heartbeat():
+        t0 = time.time()
+        while not done.wait(30):
+            sys.stderr.write(f"build.py: compiling {os.path.basename(lib)}, {time.time() - t0:.0f} s\n")
+            sys.stderr.flush()
+
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    try:
+        with concurrent.futures.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+            results = list(ex.map(compile_one, SOURCES))
+    finally:
+        done.set()
     for src, obj, cmd, r in results:
         kernels += _parse_resource_remarks(r.stderr)
         other = [ln for ln in r.stderr.splitlines() if "kernel-resource-usage" not in ln]
@@ -84,6 +102,7 @@ def build(force: bool = False, extra_flags=None, ab: bool = False) -> str:
         if r.returncode != 0:
             raise subprocess.CalledProcessError(r.returncode, cmd)
         objs.append(obj)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     tmp = lib + ".tmp"
     # libhiprtc: the bit-sliced kernels are compiled at plan time (csrc/bitslice.cpp)
     subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-lhiprtc",

@@ -193,7 +193,7 @@ struct HostBuf {
     cap = 0;
     // Non-coherent: DMA into the default (coherent, fine-grained) pinned memory ran at
     // 9 GB/s for 4 MiB D2H copies and 34-41 GB/s at 64 MiB, against 50 / 57 GB/s here
-    // (tools/host_ceilings.cpp, DESIGN.md §6.3). The host reads staging only after the
+    // (tools/host_ceilings.cpp, DESIGN.md §7.4). The host reads staging only after the
     // slot's event has completed, so coherence during the copy is never needed.
     static const unsigned flags =
         std::getenv("CALLFS_RS_PINNED_COHERENT") ? hipHostMallocDefault : hipHostMallocNonCoherent;
@@ -279,7 +279,7 @@ int pipeline_slots() {
   return v;
 }
 // Column chunk: about this many bytes over all n shards per pipeline step
-// (CALLFS_RS_CHUNK_BYTES overrides; DESIGN.md §6.3 has the sweep).
+// (CALLFS_RS_CHUNK_BYTES overrides; DESIGN.md §7.4 has the sweep).
 size_t chunk_bytes() {
   static const size_t v = [] {
     const char* e = std::getenv("CALLFS_RS_CHUNK_BYTES");
@@ -505,7 +505,7 @@ class PinnedRegistry {
 // Idle rs_host_alloc buffers kept for reuse. Page-locking a fresh buffer costs about
 // 0.2 s per 384 MiB, so a server that allocates a pinned body per request and frees it
 // after the call ran 25-30x slower than one that reuses buffers (RS(4,2) 256 MiB,
-// zero-copy: 1.6 vs 48 GiB/s encode, DESIGN.md §6.3). rs_host_free parks a buffer here;
+// zero-copy: 1.6 vs 48 GiB/s encode, DESIGN.md §7.4). rs_host_free parks a buffer here;
 // rs_host_alloc takes the smallest parked buffer that fits without wasting more than a
 // quarter of it, both sides counted in 2 MiB granules. Parked bytes are capped by
 // CALLFS_RS_HOST_POOL_BYTES (default 4 GiB;
@@ -892,7 +892,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   // Small stripes move as one contiguous row range (rows that are not inputs ride
   // along). Larger chunks move one copy per run of consecutive shard indices: each copy
   // on a stream costs ~9 us of gap, so one copy per shard was much slower than one per
-  // run (DESIGN.md §6.3).
+  // run (DESIGN.md §7.4).
   const bool coalesce = spitch <= (4u << 20);
   const std::vector<std::pair<int, int>> in_runs = index_runs(ins), out_runs = index_runs(outs);
 
@@ -901,7 +901,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   // write the caller's bytes over PCIe in one launch set over the whole call -- no
   // staging copies, no chunk pipeline, nothing for the CPU but the join of present
   // data shards. RS(10,4) 64 MiB: 43.7 GiB/s vs 36.7 for H2D + launch + D2H
-  // (tests/perf/zerocopy_probe.py, DESIGN.md §6.3).
+  // (tests/perf/zerocopy_probe.py, DESIGN.md §7.4).
   // Threshold: 48 KiB per shard over the call (S x batch), i.e. 48 KiB x n over all n
   // shards. Below it the one-dispatch path on the library's coherent staging is faster;
   // tools/zc_threshold.sh (profiles/r04/zc_threshold/zc.jsonl, GiB/s enc / dec, 1 thread,
@@ -974,7 +974,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   // inputs and writes the outputs over PCIe, one dispatch per chunk and launch group, and
   // the host spins on the kernel's completion flag. The staged path spends three dependent
   // dispatches (H2D, kernel, D2H) per chunk, which bound 4 KiB calls at ~29 us
-  // (DESIGN.md §6.3). Calls of at most CALLFS_RS_SMALL_MAX_BYTES of staging run as one
+  // (DESIGN.md §7.4). Calls of at most CALLFS_RS_SMALL_MAX_BYTES of staging run as one
   // chunk on slot 0; with CALLFS_RS_INPLACE_PIPELINE=1 (A/B) larger calls run the staged
   // path's chunk pipeline with in-place kernels instead of H2D / kernel / D2H.
   const size_t cp16 = round_up(S, 16), sp16 = cp16 * n;
@@ -1666,7 +1666,9 @@ int rs_plan_launch_ceiling_timed(rs_plan* plan, void* stream, int mode, void* st
                                  void* stop_event) {
   DeviceGuard dg;
   if (!plan || mode < 0 || mode > 8) return RS_E_ARG;
-  if (!kAbInstances && mode != 1 && mode != 2) return RS_E_UNSUPPORTED;  // (A/B build only)
+  // the product implements RS_CEIL_READ / RS_CEIL_WRITE; the other modes are the A/B build's
+  // (tools/callfs_rs_ab.h)
+  if (!kAbInstances && mode != RS_CEIL_READ && mode != RS_CEIL_WRITE) return RS_E_ARG;
   HIPCHK(hipSetDevice(plan->device));
   std::vector<int> orders;
   {
@@ -1691,7 +1693,7 @@ int rs_plan_launch_ceiling_timed(rs_plan* plan, void* stream, int mode, void* st
 
 // Times every tile order each launch group's kernel offers and keeps the fastest. Which
 // order HBM serves best varies between MI355X boxes by 1-2 points on the same shape
-// (DESIGN.md §5 "Tile order"), so a plan that is launched many times measures it on the
+// (DESIGN.md §6.2 "Tile order"), so a plan that is launched many times measures it on the
 // box it runs on, like a library autotuner, instead of trusting the rule alone. Each
 // candidate gets `reps` back-to-back launches between two events, in three rounds with the
 // candidate order rotated; the per-launch mean of the best round counts, and the rule's

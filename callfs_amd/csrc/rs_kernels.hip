@@ -508,12 +508,10 @@ bool wix_enabled() {
 }
 // Since the triple-load form (below) measured equal or faster than WIX everywhere, the
 // rule no longer takes WIX: its instances remain for rs_plan_set_orders (A/B).
-// tools/wix_ab*.sh (round 3, since removed), profiles/r03/wix/: WIX in the nibble rule's order vs the nibble kernel's
-// best order, 1 MiB shards: RS(4,2) 72.3 -> 79.0, RS(4,4) 75.0 -> 81.5, RS(5,3) 74.5 -> 79.9,
+// profiles/r03/wix/: WIX in the nibble rule's order vs the nibble kernel's best order, 1 MiB shards: RS(4,2) 72.3 -> 79.0, RS(4,4) 75.0 -> 81.5, RS(5,3) 74.5 -> 79.9,
 // RS(8,4) 76.5 -> 80.1; RS(10,4) equal, RS(16,4) / RS(20,4) / RS(32,4) -1.2 ... -1.5.
 
-// Triple loads (Policy::WIX 2): tile_order.hpp tri_rule. tools/wix_ab4.sh (round 3, since removed),
-// profiles/r03/wix/ab4_tri_verify.jsonl, % of 8 TB/s, nibble (best order) -> triples in
+// Triple loads (Policy::WIX 2): tile_order.hpp tri_rule. profiles/r03/wix/ab4_tri_verify.jsonl, % of 8 TB/s, nibble (best order) -> triples in
 // the rule's order: RS(4,2) 71.8 -> 80.6, RS(5,3) 74.6 -> 80.3, RS(8,4) 76.3 -> 80.2,
 // RS(10,4) 75.8 -> 76.6, RS(6,6) 74.6 -> 75.7, RS(8,8) 75.4 -> 76.3, RS(10,8) 74.1 -> 77.4;
 // read-only (download Verify): RS(4,2) 82.5 -> 88.4, RS(10,4) 83.8 -> 86.0 (X32). Second
@@ -527,7 +525,7 @@ bool wix_enabled() {
 // Misaligned inputs with 16-B-aligned outputs (upstream Split of an io.ReadAll body: the
 // data shards inside the body, the parity in AllocAligned buffers): the triple form with
 // unaligned 16-B loads, X32 up to 256 tiles per stripe and X8 above, not the realigning
-// kernel. tools/unaligned_tri_probe.sh (profiles/r04/utri1/readall_enc.jsonl, % of 8 TB/s,
+// kernel. profiles/r04/utri1/readall_enc.jsonl (% of 8 TB/s,
 // realigning kernel (rule) -> triples in X32 / X8): RS(10,4) 104,858 B 69.5 -> 76.7 (G2
 // 77.5), RS(12,4) 87,382 B 69.0 -> 75.7, RS(5,3) 209,716 B 71.0 -> 78.3, RS(6,3) 174,763 B
 // 70.6 -> 74.4, RS(10,8) 1,048,577 B 68.8 -> 70.9, RS(10,4) 6,710,887 B 71.2 -> 72.8 (X8),
@@ -614,7 +612,7 @@ bool takes_realign_tri(const ApplyArgs& a) {
 
 // The realigning kernel's tile order (index into kLdsRealignOut): a tuned realign code
 // (kOrderRealign + TileOrder) names it; otherwise CALLFS_RS_TILE_ORDER=consecutive / x8
-// / x32, else X32 (DESIGN.md §5 "XCD-grouped tile orders": tools/order_ab.py, Split
+// / x32, else X32 (tools/order_ab.py, Split
 // layout, % of 8 TB/s, two runs, consecutive -> X32: RS(10,4) 64 MiB objects 68.3 /
 // 68.6 -> 69.5 / 69.9, RS(4,2) 1,048,577 B 67.1 / 66.8 -> 68.6 / 68.3, RS(12,4) S =
 // 5,592,406 65.5 / 65.9 -> 66.9 / 66.9, the other five shapes -0.2 ... +0.9).
@@ -1043,7 +1041,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
 // ---- no-lookup ceiling (measurement only; rs_plan_launch_ceiling) ----------------------
 // Policy::NOMATH turns the LDS kernel into the memory ceiling of its own traffic shape:
 // the same loads, stores, grid, block size, tile order and table prologue, with the
-// lookups replaced by one XOR per input dword (DESIGN.md §5 "Traffic ceiling per shape").
+// lookups replaced by one XOR per input dword.
 // bench.py times it in the same process as the plan it bounds.
 namespace {
 #if CALLFS_RS_AB_INSTANCES

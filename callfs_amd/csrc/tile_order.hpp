@@ -1,4 +1,4 @@
-// Tile order of the RS kernels (DESIGN.md §5 "Tile order"): which column tile of which
+// Tile order of the RS kernels (DESIGN.md §6.2 "Tile order"): which column tile of which
 // stripe block t works on (map_tile, host and device), and the measured rules that pick
 // the order for a launch (lds_tile_order, wide_tile_order, vec_tile_order; host).
 // Plain C++ apart from the __host__ __device__ marker, so tests/native/host_test.cpp
@@ -341,7 +341,7 @@ inline bool tri_rule(int K, int R, bool misaligned, bool verify, bool read_only,
                         TileOrder::kConsecutive) >= 0;
 }
 // Triple loads in the realigning kernel (misaligned shards, upstream Split layout):
-// measured in round 4 (DESIGN.md §5 "Shard triples"); until then only rs_plan_tune and
+// measured in round 4; until then only rs_plan_tune and
 // rs_plan_set_orders take it.
 inline bool realign_tri_rule(int K, int R, bool verify, bool read_only) {
   (void)K; (void)R; (void)verify; (void)read_only;

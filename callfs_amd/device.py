@@ -196,11 +196,12 @@ class Plan:
     CEILINGS = {"nolookup": 0, "read": 1, "write": 2, "write64": 3, "write128": 4,
                 "write256": 5, "read64": 6, "read128": 7, "read256": 8}
 
-    def launch_ceiling(self, mode: str = "nolookup",
+    def launch_ceiling(self, mode: str = "read",
                        stream: Optional[torch.cuda.Stream] = None, events=None) -> None:
-        """rs_plan_launch_ceiling (measurement only): this plan's traffic as the kernel's
-        no-lookup form, or its read / write streams alone, same grid and tile order.
-        "nolookup" and "write" leave junk in the written shards. events: as for launch()."""
+        """rs_plan_launch_ceiling (measurement only): this plan's read / write streams
+        alone, same grid and tile order ("write" leaves junk in the written shards). The
+        A/B build (CALLFS_RS_LIB) adds "nolookup" (the kernel's no-lookup form) and the
+        aligned-window probes; the product refuses them (RS_E_ARG). events: as for launch()."""
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         if events is None:
             N.check(N.lib.rs_plan_launch_ceiling(self.handle, ctypes.c_void_p(s.cuda_stream),

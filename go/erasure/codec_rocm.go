@@ -34,7 +34,7 @@ var (
 	gpuCtx  *C.rs_ctx // nil: no usable device, every call takes the CPU codec
 	// CALLFS_ERASURE__GPU_MIN_BYTES: objects below this stay on the CPU codec
 	// (INTEGRATION.md "when the GPU pays"). 64 MiB is where one GPU call passes one CPU
-	// thread on the round-4 build (DESIGN.md §6.3 "CPU or GPU", tools/crossover_r04.sh,
+	// thread on the round-4 build (DESIGN.md §7.4 "CPU or GPU", tools/crossover_r04.sh,
 	// profiles/r04/crossover/): RS(10,4) 23.8 vs 19.5 GiB/s from pageable buffers, RS(4,2)
 	// 43.0 vs 34.8 and RS(10,4) 37.8 vs 19.5 from rs_host_alloc buffers; one threshold for
 	// every profile (RS(4,2) on pageable buffers stays within 6 % of the CPU above it).
@@ -103,7 +103,7 @@ func decodeErr(rc C.int) error {
 // slices (C memory: cgo's pointer rules and runtime.Pinner do not apply to it, and the GC
 // never moves it). When every shard of a call lies inside such buffers, the library runs
 // the call zero-copy: H2D, kernels and D2H straight on these bytes, no CPU copy through its
-// staging (include/callfs_rs.h rs_host_alloc; DESIGN.md §6.3, 38-45 GiB/s for objects of
+// staging (include/callfs_rs.h rs_host_alloc; DESIGN.md §7.4, 38-45 GiB/s for objects of
 // 10 MiB and up on one request thread). Upload bodies read into a BodyBuffer instead of
 // io.ReadAll's heap slice (post_file_enhanced.go:125-127) and shards fetched into
 // HostBuffers instead of io.ReadAll (manager.go:473,530) take that path. Release each with
@@ -246,7 +246,11 @@ func (c *Codec) Decode(shards [][]byte, profile ErasureProfile, originalSize int
 // into HostBuffer(S) instead of io.ReadAll): the reconstructed entries it fills and the
 // object it returns are HostBuffers too, so the whole call runs zero-copy. The caller
 // releases the returned object and every shard entry with FreeHostBuffer once the response
-// is written. Without a device it is Decode (heap buffers, FreeHostBuffer ignores them).
+// is written -- on the ErrShardCorrupted and ErrInsufficientShards paths as well: there
+// Reconstruct has run and the nil entries are filled with HostBuffers, as upstream fills
+// them (codec.go:55), so the caller owns and frees them. Every other error leaves the
+// caller's slice untouched and frees what the call allocated. Without a device it is
+// Decode (heap buffers, FreeHostBuffer ignores them).
 // Not in the reference API: an addition for servers that read into pinned buffers.
 func (c *Codec) DecodePinned(shards [][]byte, profile ErasureProfile, originalSize int64) ([]byte, error) {
 	return c.decode(shards, profile, originalSize, true)

@@ -186,7 +186,7 @@ void rs_plan_destroy(rs_plan* plan);
 #define RS_ORDER_GROUP2 2
 #define RS_ORDER_SEG8 3
 #define RS_ORDER_SEG16 4
-/* consecutive tiles, J = 8 / 32 of them per XCD in turn (DESIGN.md §5 "XCD-grouped") */
+/* consecutive tiles, J = 8 / 32 of them per XCD in turn */
 #define RS_ORDER_XCD8 5
 #define RS_ORDER_XCD32 6
 /* misaligned shards (upstream Split layout at odd S): the kernel that realigns loads and
@@ -212,26 +212,14 @@ int  rs_plan_forms(const rs_plan* plan, int* forms, int max_groups);
 /* Measurement only (no upstream counterpart): enqueues the plan's launch groups as a
  * traffic ceiling of the same shape, on the production grid, tile order and slicing, for
  * a roofline denominator measured in the same process (bench.py):
- *   RS_CEIL_NOLOOKUP  the production kernel's no-lookup form: the same loads, stores and
- *                     table prologue, one XOR per input dword in place of the lookups;
  *   RS_CEIL_READ      the plan's read streams alone (k inputs + compared rows);
- *   RS_CEIL_WRITE     its write streams alone.
- * NOLOOKUP and WRITE leave junk in the written shards and NOLOOKUP may flag status:
- * relaunch the plan (and read rs_plan_status) before relying on either.
- * The product library implements READ and WRITE; NOLOOKUP and the probes below exist in
- * the A/B build of the tools (libcallfs_rs_ab.so) and return RS_E_UNSUPPORTED here. */
-#define RS_CEIL_NOLOOKUP 0
+ *   RS_CEIL_WRITE     its write streams alone (leaves junk in the written shards:
+ *                     relaunch the plan before relying on them).
+ * Any other mode returns RS_E_ARG. (The development tools' A/B build, built on demand with
+ * `python callfs_amd/build.py --ab`, adds the kernel's no-lookup form and aligned-window
+ * probes: tools/callfs_rs_ab.h.) */
 #define RS_CEIL_READ 1
 #define RS_CEIL_WRITE 2
-/* probes: the write streams alone from each row's first 64 / 128 / 256-B boundary on
- * (every wave's 1 KiB store aligned to that; consecutive tiles) */
-#define RS_CEIL_WRITE_AL64 3
-#define RS_CEIL_WRITE_AL128 4
-#define RS_CEIL_WRITE_AL256 5
-/* probes: the read streams alone from each shard's first 64 / 128 / 256-B boundary on */
-#define RS_CEIL_READ_AL64 6
-#define RS_CEIL_READ_AL128 7
-#define RS_CEIL_READ_AL256 8
 int  rs_plan_launch_ceiling(rs_plan* plan, void* stream, int mode);
 /* The same, with its kernels timed as rs_plan_launch_timed times the plan's. */
 int  rs_plan_launch_ceiling_timed(rs_plan* plan, void* stream, int mode, void* start_event,

@@ -27,6 +27,17 @@ def test_exports_every_declared_symbol(native_lib):
     assert set(names) == set(native_lib.SIGNATURES), "ctypes table out of sync with header"
 
 
+def test_product_header_declares_only_product_modes():
+    """Verdict r05 item 6: the product header declares only what the product implements;
+    the A/B build's measurement modes live in a tools-only header."""
+    text = open(HEADER).read()
+    for name in ("RS_CEIL_NOLOOKUP", "RS_CEIL_WRITE_AL", "RS_CEIL_READ_AL"):
+        assert name not in text, name
+    assert "#define RS_CEIL_READ 1" in text and "#define RS_CEIL_WRITE 2" in text
+    ab = open(os.path.join(ROOT, "tools", "callfs_rs_ab.h")).read()
+    assert "#define RS_CEIL_NOLOOKUP 0" in ab
+
+
 def test_abi_version(native_lib):
     assert native_lib.lib.rs_abi_version() == 1
 

@@ -3,7 +3,9 @@
 # (tools/order_ab.py, planar layout). Usage: bash tools/dma_probe.sh <tag>
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; TAG="${1:-dma}"; O="$R/gpurun_out/$TAG"; mkdir -p "$O"; cd "$R"
-export CALLFS_RS_LIB="$R/callfs_amd/libcallfs_rs_ab.so"
+# the A/B build is not pushed: built here on demand (build/ab/, tools/callfs_rs_ab.h)
+timeout -k 10 900 python3 callfs_amd/build.py --ab > /dev/null || exit $?
+export CALLFS_RS_LIB="$R/build/ab/libcallfs_rs_ab.so"
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
   tests/test_gpu_parity.py -k every_offered > "$O/pytest_ab.log" 2>&1 || exit $?
 echo "ab tests ok"

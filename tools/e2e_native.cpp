@@ -11,7 +11,7 @@
 // rs_reconstruct_batch (verify on) plus the per-object join copy.
 // CALLFS_E2E_PINNED=1: every buffer comes from rs_host_alloc (the server reading bodies
 // and shards into pinned memory), so calls take the zero-copy direct-DMA path.
-// Zero-copy concurrency probes (DESIGN.md §6.3):
+// Zero-copy concurrency probes (DESIGN.md §7.4):
 // CALLFS_E2E_EXTRA_PINNED_MIB=N: also hold N MiB of touched, unused rs_host_alloc memory
 //   (a larger pinned footprint without more concurrent calls);
 // CALLFS_E2E_SERIAL=1: one rs_* call at a time across all threads (concurrency without

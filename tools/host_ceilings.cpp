@@ -1,7 +1,7 @@
 // Host-side transfer ceilings for the host-memory RS path (development tool, not
 // product): pinned H2D / D2H / both directions at once, H2D straight from pageable
 // memory, hipHostRegister cost, and pageable<->pinned memcpy with T threads.
-// They bound tools/e2e_native's end-to-end rates (DESIGN.md §6.3).
+// They bound tools/e2e_native's end-to-end rates (DESIGN.md §7.4).
 //
 // build: hipcc -O2 -std=c++17 tools/host_ceilings.cpp -lpthread -o tools/host_ceilings
 // run:   tools/host_ceilings [MiB=64] [reps=20]

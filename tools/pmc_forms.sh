@@ -3,7 +3,9 @@
 # Usage: bash tools/pmc_forms.sh <tag> <shape> <order> [<order> ...]
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; TAG="$1"; SH="$2"; shift 2; OUT="$R/gpurun_out/$TAG"; mkdir -p "$OUT"
-export CALLFS_RS_LIB="$R/callfs_amd/libcallfs_rs_ab.so"
+# the A/B build is not pushed: built here on demand (build/ab/, tools/callfs_rs_ab.h)
+timeout -k 10 900 python3 callfs_amd/build.py --ab > /dev/null || exit $?
+export CALLFS_RS_LIB="$R/build/ab/libcallfs_rs_ab.so"
 cd /tmp && export TMPDIR=/tmp
 PA="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
 PB="GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"

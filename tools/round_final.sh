@@ -18,13 +18,14 @@ timeout -k 10 300 tools/write_pattern 6 > "gpurun_out/$TAG/write_pattern_bs.csv"
 echo "write pattern ok"
 # the double-buffered triples with 4 / 8 stripes interleaved (A/B build): bit-exact, then
 # against the rule's tri-G2 on the bench shape and its neighbours
-CALLFS_RS_LIB="$R/callfs_amd/libcallfs_rs_ab.so" timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 \
+timeout -k 10 900 python3 callfs_amd/build.py --ab > /dev/null || exit $?
+CALLFS_RS_LIB="$R/build/ab/libcallfs_rs_ab.so" timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 \
   --timeout-method thread -m gpu tests/test_gpu_parity.py -k every_offered > "gpurun_out/$TAG/pytest_ab.log" 2>&1 || exit $?
 echo "ab tests ok"
 A=()
 for s in 10,4,1048576,256 10,4,1048576,512 16,4,1048576,256 8,4,2097152,128 12,4,1398102,128 10,4,104858,1024 6,3,174763,2048; do
   A+=(--shape "$s,-,planar")
 done
-CALLFS_RS_LIB="$R/callfs_amd/libcallfs_rs_ab.so" timeout -k 10 600 python3 -u tools/order_ab.py --rounds 3 \
+CALLFS_RS_LIB="$R/build/ab/libcallfs_rs_ab.so" timeout -k 10 600 python3 -u tools/order_ab.py --rounds 3 \
   --orders tri-g2,tridb-g4,tridb-g8,tri-x32 "${A[@]}" > "gpurun_out/$TAG/tridb_g.jsonl" 2>&1 || exit $?
 echo "tridb-g ok"
