@@ -34,10 +34,10 @@ var (
 	gpuCtx  *C.rs_ctx // nil: no usable device, every call takes the CPU codec
 	// CALLFS_ERASURE__GPU_MIN_BYTES: objects below this stay on the CPU codec
 	// (INTEGRATION.md "when the GPU pays"). 64 MiB is where one GPU call passes one CPU
-	// thread on the round-4 build (DESIGN.md §7.4 "CPU or GPU", tools/crossover_r04.sh,
-	// profiles/r04/crossover/): RS(10,4) 23.8 vs 19.5 GiB/s from pageable buffers, RS(4,2)
-	// 43.0 vs 34.8 and RS(10,4) 37.8 vs 19.5 from rs_host_alloc buffers; one threshold for
-	// every profile (RS(4,2) on pageable buffers stays within 6 % of the CPU above it).
+	// thread on the round-6 build (DESIGN.md §7.4 "CPU or GPU", tools/n1_r06.sh,
+	// profiles/r06/n1/): RS(10,4) 28.2 vs 20.0 GiB/s from pageable buffers and 33.0 through
+	// pinned bodies (BodyBuffer), RS(4,2) 34.7 vs 29.3 through pinned bodies; at 16 MiB the
+	// cache-resident CPU port leads (51-53 vs 20-33); one threshold for every profile.
 	gpuMinBytes = envInt("CALLFS_ERASURE__GPU_MIN_BYTES", 64<<20)
 )
 

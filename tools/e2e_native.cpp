@@ -17,6 +17,13 @@
 // CALLFS_E2E_SERIAL=1: one rs_* call at a time across all threads (concurrency without
 //   overlap: same footprint, calls serialised by a mutex in this harness);
 // CALLFS_E2E_FRESH=1: allocate (and free) the output buffers of every call anew.
+// CALLFS_E2E_BODY=1: the shim's pinned-body path exactly as tests/native/cgo_drive.c drives
+//   it (codec_rocm.go BodyBuffer -> Encode, DecodePinned, FreeHostBuffer): each encode takes a
+//   body of n*S bytes from rs_host_alloc (the context's pool after the first call), holding
+//   the object in its first L bytes as io.ReadFull left it, zeroes the spare capacity as Split
+//   does, encodes in place with rs_encode and frees the body; each decode allocates the lost
+//   shards' and the object's buffers from rs_host_alloc, runs rs_codec_decode and frees them
+//   (the fetched shards are pinned buffers filled once).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -87,6 +94,7 @@ int main(int argc, char** argv) {
     }
   }
   const bool encoder_api = std::getenv("CALLFS_E2E_ENCODER") != nullptr;
+  const bool body_api = std::getenv("CALLFS_E2E_BODY") != nullptr;
   const int nb = std::getenv("CALLFS_E2E_BATCH") ? std::atoi(std::getenv("CALLFS_E2E_BATCH")) : 0;
   rs_ctx* ctx = nullptr;
   if (rs_init(&ctx, 0) != RS_OK) {
@@ -94,7 +102,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   g_ctx = ctx;
-  g_pinned = std::getenv("CALLFS_E2E_PINNED") != nullptr;
+  g_pinned = std::getenv("CALLFS_E2E_PINNED") != nullptr || body_api;
   const size_t S = (L + k - 1) / k;
   const bool serial = std::getenv("CALLFS_E2E_SERIAL") != nullptr;
   const bool fresh = std::getenv("CALLFS_E2E_FRESH") != nullptr;
@@ -182,6 +190,45 @@ int main(int argc, char** argv) {
               }
               if (b == 0) me.out = bjoin;
             }
+          } else if (encode && body_api) {
+            uint8_t* body = nullptr;
+            rc = rs_host_alloc(ctx, n * S, reinterpret_cast<void**>(&body));
+            if (rc == RS_OK) {
+              // the body as io.ReadFull leaves it: the object's L bytes (written once per
+              // thread into the first body; a pool body holds the last request's object)
+              if (me.ops == 0) std::memcpy(body, me.src.data(), L);
+              std::memset(body + L, 0, n * S - L);  // Split zeroes the spare capacity
+              std::vector<const uint8_t*> dptr(k);
+              std::vector<uint8_t*> pptr(m);
+              for (int i = 0; i < k; ++i) dptr[i] = body + S * i;
+              for (int j = 0; j < m; ++j) pptr[j] = body + S * (k + j);
+              rc = rs_encode(ctx, k, m, S, dptr.data(), pptr.data());
+              if (rs_host_free(ctx, body) != RS_OK && rc == RS_OK) rc = RS_E_ARG;
+            }
+          } else if (!encode && body_api) {
+            // DecodePinned: the lost entries and the object come from rs_host_alloc per call
+            std::vector<void*> mine;
+            rc = RS_OK;
+            for (int i = 0; i < n && rc == RS_OK; ++i) {
+              bool gone = false;
+              for (int e : erase) gone |= e == i;
+              lens[i] = gone ? 0 : S;
+              ptrs[i] = me.sh[i].data();
+              if (gone) {
+                void* b = nullptr;
+                rc = rs_host_alloc(ctx, S, &b);
+                ptrs[i] = static_cast<uint8_t*>(b);
+                mine.push_back(b);
+              }
+            }
+            void* ob = nullptr;
+            if (rc == RS_OK) rc = rs_host_alloc(ctx, L, &ob);
+            if (rc == RS_OK)
+              rc = rs_codec_decode(ctx, k, m, ptrs.data(), lens.data(), static_cast<uint8_t*>(ob),
+                                   static_cast<int64_t>(L));
+            if (rc == RS_OK && me.ops == 0) std::memcpy(me.out.data(), ob, L);
+            if (ob) mine.push_back(ob);
+            for (void* b : mine) rs_host_free(ctx, b);
           } else if (encode && encoder_api) {
             // Split as upstream: full data shards alias src, the tail shard is a
             // zero-padded copy, parity lands in fresh buffers
@@ -235,6 +282,7 @@ int main(int argc, char** argv) {
               "\"batch\": %d, \"erase_count\": %zu, \"encode_gib_s\": %.3f, \"decode_gib_s\": %.3f, "
               "\"encode_calls\": %ld, \"decode_calls\": %ld, \"ok\": %s}\n",
               nb > 0 ? (g_pinned ? "native-batch-pinned" : "native-batch")
+                     : body_api ? "native-body-pinned"
                      : encoder_api ? (g_pinned ? "native-encoder-pinned" : "native-encoder")
                                    : (g_pinned ? "native-pinned" : "native"),
               k, m, L, T, nb > 0 ? nb : 1, erase.size(), e.first, d.first, e.second, d.second,
