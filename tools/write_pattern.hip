@@ -9,6 +9,8 @@
 // build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/write_pattern.hip -o tools/write_pattern
 // run:   tools/write_pattern [reps] [pitch]   (pitch: rows of 1 MiB shards at 1, 2, 6.4
 //         and 8 MiB pitch, then 6.4 MiB shards; does the written span's contiguity matter?)
+//        tools/write_pattern [reps] burst   (each block writes U = 1, 2, 4 or 8 consecutive 8 KiB
+//         pieces of every row: each row front advances 8-64 KiB per block; verdict r05 item 7)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -41,6 +43,8 @@ struct Args {
   uint32_t split;   // 1: each block stores ONE of the R rows of its tile; the R blocks of a
                     // tile are neighbours in launch order (the same rows in flight chip-wide
                     // as R-row blocks, one row per block)
+  uint32_t burst;   // U >= 1: a block's tile is U * blockDim * 16 bytes of every row, each lane
+                    // storing U vectors per row (wave w's stores cover 1 KiB pieces w, w + nw, ...)
   uint32_t* sink;
 };
 
@@ -64,9 +68,19 @@ __global__ __launch_bounds__(1024) void pattern(Args a) {
   const uint32_t x = t * 0x9E3779B1u + threadIdx.x;
   u32x4 acc = {0, 0, 0, 0};
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const uint64_t tb = blockDim.x * 16ull;  // tile bytes per row
-  for (uint32_t i = 0; i < a.R; ++i) {
+  const uint32_t U = a.burst ? a.burst : 1;
+  const uint64_t tb = blockDim.x * 16ull * U;  // tile bytes per row
+  for (uint32_t i = 0; i < a.R * U; ++i) {
     if (a.split && i != only) continue;
+    if (U > 1) {  // burst: row i / U, the u-th run of nw pieces of the row's tile
+      const uint32_t r = i / U, u = i % U;
+      uint8_t* row = a.base + (static_cast<uint64_t>(stripe) * a.R + r) * a.pitch +
+                     static_cast<uint64_t>(tile) * tb;
+      u32x4* p = reinterpret_cast<u32x4*>(row + (u * nw + w) * 1024ull) + lane;
+      const u32x4 v = {x, x + r, x ^ r, u};
+      __builtin_nontemporal_store(v, p);
+      continue;
+    }
     // piece f of the block's nw*R 1 KiB pieces: row f / nw, piece f % nw of the row's tile
     const uint32_t f = a.rowwave ? w * a.R + i : i * nw + w;
     const uint32_t r = f / nw, piece = f % nw;
@@ -102,10 +116,21 @@ int main(int argc, char** argv) {
     uint32_t R, order, g, read, rowwave, bs;
     uint64_t pitch;  // 0: S
     uint32_t split;
+    uint32_t burst;
   };
   std::vector<V> vs;
   const uint64_t shapes[] = {1ull << 20, 2ull << 20, 6710912, 8ull << 20, 64ull << 20};
-  if (argc > 2 && argv[2][0] == 's') {
+  if (argc > 2 && argv[2][0] == 'b') {
+    // each row front advancing U * 8 KiB per block (512 threads), R = 4 and 8 rows
+    for (int rep = 0; rep < 2; ++rep)
+      for (uint64_t S : {1ull << 20, 6710912ull})
+        for (uint32_t R : {4u, 8u})
+          for (uint32_t U : {1u, 2u, 4u, 8u}) {
+            vs.push_back({"consecutive", S, R, 0, 0, 0, 0, 512, 0, 0, U});
+            vs.push_back({"G8", S, R, 1, 8, 0, 0, 512, 0, 0, U});
+            vs.push_back({"Q8", S, R, 2, 8, 0, 0, 512, 0, 0, U});
+          }
+  } else if (argc > 2 && argv[2][0] == 's') {
     // one row per block against R rows per block, same rows in flight (split probe)
     for (int rep = 0; rep < 2; ++rep)
       for (uint64_t S : {1ull << 20, 6710912ull})
@@ -136,13 +161,13 @@ int main(int argc, char** argv) {
           vs.push_back({"Q8", S, R, 2, 8, 0, 0, bs, 0});
         }
   }
-  std::printf("variant,shard_bytes,pitch,rows,block,mode,split,GBps\n");
+  std::printf("variant,shard_bytes,pitch,rows,block,mode,split,burst,GBps\n");
   for (const V& v : vs) {
     Args a{};
     a.base = buf;
     a.pitch = v.pitch ? v.pitch : v.S;
     a.R = v.R;
-    const uint64_t tb = v.bs * 16ull;
+    const uint64_t tb = v.bs * 16ull * (v.burst ? v.burst : 1);
     a.tps = static_cast<uint32_t>(v.S / tb);
     a.batch = static_cast<uint32_t>(total / (a.pitch * v.R));
     a.order = v.order;
@@ -151,6 +176,7 @@ int main(int argc, char** argv) {
     a.rowwave = v.rowwave;
     a.sink = sink;
     a.split = v.split;
+    a.burst = v.burst;
     uint32_t grid = a.tps * a.batch * (v.split ? v.R : 1);
     if (v.order == 3) {
       a.tps = 1;
@@ -169,9 +195,9 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       best = ms < best ? ms : best;
     }
-    std::printf("%s,%llu,%llu,%u,%u,%s,%u,%.0f\n", v.name, static_cast<unsigned long long>(v.S),
+    std::printf("%s,%llu,%llu,%u,%u,%s,%u,%u,%.0f\n", v.name, static_cast<unsigned long long>(v.S),
                 static_cast<unsigned long long>(a.pitch), v.R, v.bs, v.read ? "read" : "write",
-                v.split, bytes / (best * 1e-3) / 1e9);
+                v.split, v.burst ? v.burst : 1, bytes / (best * 1e-3) / 1e9);
     std::fflush(stdout);
   }
   CK(hipFree(buf));
