@@ -276,11 +276,12 @@ def plan_ceilings(enc, dec, stream):
     for name, plan in (("decode", dec), ("encode", enc)):
         ms = {mode: _launch_ms(lambda evs: plan.launch_ceiling(mode, stream, events=evs), stream)
               for mode in ("read", "write")}
-        try:  # the no-lookup form: A/B build of the library only (CALLFS_RS_LIB)
+        try:  # the no-lookup form: A/B build of the library only (CALLFS_RS_LIB); the
+            # product refuses the mode (RS_E_ARG: tools/callfs_rs_ab.h)
             ms["nolookup"] = _launch_ms(
                 lambda evs: plan.launch_ceiling("nolookup", stream, events=evs), stream)
         except N.NativeError as e:
-            if e.code != N.RS_E_UNSUPPORTED:
+            if e.code != N.RS_E_ARG:
                 raise
         plan.corrupt(stream)  # the no-lookup form's Verify rows compare junk: clear
         plan.launch(stream)

@@ -84,6 +84,8 @@ SIGNATURES = {
     "rs_plan_bytes": (ctypes.c_uint64, [_vp]),
     "rs_plan_groups": (ctypes.c_int, [_vp]),
     "rs_plan_forms": (_int, [_vp, ctypes.POINTER(_int), _int]),
+    "rs_tune_table_reset": (_int, [ctypes.c_char_p]),
+    "rs_tune_table_entries": (_int, []),
     "rs_plan_launch_ceiling": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "rs_plan_launch_ceiling_timed": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp, _vp]),
     "rs_plan_destroy": (None, [_vp]),

@@ -27,7 +27,7 @@ LIB_AB = os.path.join(os.path.dirname(HERE), "build", "ab", "libcallfs_rs_ab.so"
 # kernel's speed depends on its waves per SIMD.
 RESOURCES = os.path.join(HERE, "kernel_resources.json")
 SOURCES = ["rs_kernels.hip", "sha256.hip", "rs_capi.cpp", "bitslice.cpp"]
-HEADERS = ["bitslice.hpp", "bitslice_gen.hpp", "rs_kernels.hpp", "rs_apply.hpp", "tile_order.hpp", "gf256.hpp", "copy_pool.hpp", "dispatch.hpp", "sha256.hpp", os.path.join("..", "..", "include", "callfs_rs.h")]
+HEADERS = ["bitslice.hpp", "bitslice_gen.hpp", "bitslice_rule.hpp", "tune_table.hpp", "rs_kernels.hpp", "rs_apply.hpp", "tile_order.hpp", "gf256.hpp", "copy_pool.hpp", "dispatch.hpp", "sha256.hpp", os.path.join("..", "..", "include", "callfs_rs.h")]
 ARCH = os.environ.get("CALLFS_OFFLOAD_ARCH", "gfx950")
 
 

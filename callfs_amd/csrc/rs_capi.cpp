@@ -37,6 +37,7 @@
 #include "gf256.hpp"
 #include "rs_kernels.hpp"
 #include "sha256.hpp"
+#include "tune_table.hpp"
 
 using namespace callfs;
 
@@ -439,12 +440,15 @@ hipError_t launch_groups(const Tables& t, const MetaLayout& L, int batch, uint8_
                          const std::vector<int>* orders = nullptr, LaunchEvents ev = {}) {
   const size_t ng = t.groups.size();
   for (size_t gi = 0; gi < ng; ++gi) {
-    const int order = orders && gi < orders->size() ? (*orders)[gi] : -1;
+    const ApplyArgs a = group_args(t, L, gi, batch, d, S, status_stride, hint);
+    // a plan's pinned or tuned order; else what rs_plan_tune measured for this shape on the
+    // device (tune_table.hpp); else the rule
+    int order = orders && gi < orders->size() ? (*orders)[gi] : -1;
+    if (order < 0) order = tuned_order(a);
     LaunchEvents g;
     g.start = gi == 0 ? ev.start : nullptr;
     g.stop = gi + 1 == ng ? ev.stop : nullptr;
-    hipError_t e = launch_apply(group_args(t, L, gi, batch, d, S, status_stride, hint), s,
-                                /*bytes_only=*/false, order, g);
+    hipError_t e = launch_apply(a, s, /*bytes_only=*/false, order, g);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -1788,6 +1792,7 @@ int rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_gro
     for (size_t c = 1; c < cand.size(); ++c)
       if (best[c] < best[win] * (win == 0 ? 1.0f - tune_bar() / 100.0f : 1.0f)) win = c;
     chosen[gi] = cand[win];
+    record_tuned(a, chosen[gi]);  // later untuned launches of this shape take it
     if (tune_log()) {
       std::fprintf(stderr, "rs_plan_tune: group %zu (K=%d R=%d S=%zu batch=%d):", gi, a.K, a.R,
                    static_cast<size_t>(a.S), a.batch);
@@ -1829,6 +1834,13 @@ int rs_plan_set_orders(rs_plan* plan, const int* orders, int n) {
   plan->orders = next;
   return RS_OK;
 }
+
+int rs_tune_table_reset(const char* path) {
+  tune_table().reset(path);
+  return RS_OK;
+}
+
+int rs_tune_table_entries(void) { return static_cast<int>(tune_table().size()); }
 
 int rs_plan_forms(const rs_plan* plan, int* forms, int max_groups) {
   if (!plan || max_groups < 0 || (max_groups > 0 && !forms)) return RS_E_ARG;

@@ -13,9 +13,11 @@
 #include <hip/hip_ext.h>
 
 #include "bitslice.hpp"
+#include "bitslice_rule.hpp"
 #include "dispatch.hpp"
 #include "rs_apply.hpp"
 #include "tile_order.hpp"
+#include "tune_table.hpp"
 
 namespace callfs {
 
@@ -662,7 +664,38 @@ int bitslice_order(TileOrder o) {
 
 bool bitslice_wanted(const ApplyArgs& a) { return takes_bitslice(a); }
 
+namespace {
+TuneKey key_of(const ApplyArgs& a) {
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) device = 0;
+  const uint32_t rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
+  return tune_key(device, a.K, a.R, (a.S / 16 + LdsPolicy::BS - 1) / LdsPolicy::BS, a.addr_tz,
+                  (a.verify_mask & rows) != 0, (a.verify_mask & rows) == rows, a.in_misalign != 0,
+                  a.out_misalign != 0);
+}
+}  // namespace
+
+int tuned_order(const ApplyArgs& a) {
+  TuneTable& t = tune_table();
+  if (t.empty()) return -1;
+  const int o = t.lookup(key_of(a));
+  if (o < 0) return -1;
+  const std::vector<int> c = order_candidates(a, /*every_instance=*/true);
+  if (std::find(c.begin(), c.end(), o) == c.end()) return -1;
+  if (o >= kOrderBitslice) {  // host calls never wait for a compile: the rule until it is ready
+    auto* k = static_cast<bs::Kernel*>(const_cast<void*>(a.bs));
+    if (k->state() != bs::Kernel::State::kReady) {
+      k->compile_async();
+      return -1;
+    }
+  }
+  return o;
+}
+
+void record_tuned(const ApplyArgs& a, int order) { tune_table().record(key_of(a), order); }
+
 int launch_form(const ApplyArgs& a, int order) {
+  if (order < 0) order = tuned_order(a);
   if (order >= 0) return order;
   if (takes_bitslice(a) && static_cast<const bs::Kernel*>(a.bs)->state() == bs::Kernel::State::kReady)
     return kOrderBitslice + static_cast<int>(bitslice_rule_order(a));

@@ -170,8 +170,15 @@ std::vector<int> order_candidates(const ApplyArgs& a, bool every_instance = fals
 bool bitslice_wanted(const ApplyArgs& a);
 
 // The form (an order code as order_candidates lists them) launch_apply runs for `order`
-// (-1 = the rule, whose bit-sliced choice counts once its kernel is compiled).
+// (-1 = the tune table's entry for the launch's shape, else the rule, whose bit-sliced choice
+// counts once its kernel is compiled).
 int launch_form(const ApplyArgs& a, int order);
+
+// The tune table (tune_table.hpp): the order rs_plan_tune measured for launch `a`'s shape on
+// the current device, when it is one `a` offers and (for a bit-sliced order) its kernel is
+// compiled -- else -1, and the rule decides. record_tuned stores a tuner's choice.
+int tuned_order(const ApplyArgs& a);
+void record_tuned(const ApplyArgs& a, int order);
 
 // Measurement only (rs_plan_launch_ceiling), for launch `a` in the order the production
 // launch takes (`order` as for launch_apply), on the production grid and slicing:

@@ -209,6 +209,15 @@ int  rs_plan_set_orders(rs_plan* plan, const int* orders, int n);
  * where the rule gives the group the bit-sliced kernel; the codes rs_plan_tune reports).
  * Returns the number of launch groups, or RS_E_ARG. */
 int  rs_plan_forms(const rs_plan* plan, int* forms, int max_groups);
+/* The tune table: every rs_plan_tune records its choice per launch shape
+ * (device, k, rows, tiles-per-stripe bucket, address alignment, written / compared rows,
+ * misalignment), and launches with no order of their own -- untuned plans, the host-memory
+ * calls -- take the recorded form for their shape before the built-in rule. With
+ * CALLFS_RS_TUNE_TABLE=<file> the table is read from and written back to that file, so a
+ * box is tuned once. rs_tune_table_reset forgets every entry and binds the table to `path`
+ * (NULL: CALLFS_RS_TUNE_TABLE, or memory only); rs_tune_table_entries counts them. */
+int  rs_tune_table_reset(const char* path);
+int  rs_tune_table_entries(void);
 /* Measurement only (no upstream counterpart): enqueues the plan's launch groups as a
  * traffic ceiling of the same shape, on the production grid, tile order and slicing, for
  * a roofline denominator measured in the same process (bench.py):

@@ -11,6 +11,8 @@
 //     round-robin device slots, split ways and column part boundaries
 //  7. per-device kernel setup (DeviceOnce): the wide kernels' dynamic-LDS opt-in is issued
 //     once per (device, R), before the first such launch on each device
+//  9. the tune table (tune_table.hpp): shape keys, lookup and rule fallback, replacement,
+//     persistence through a file, and concurrent recording and lookups
 //  8. the bit-sliced kernels' generator (bitslice_gen.hpp): the bit transpose against its
 //     definition, each coefficient's GF(2) matrix against the field, the XOR network of
 //     random coefficient blocks (zeros included) against a scalar GF multiply, the rule
@@ -22,12 +24,16 @@
 #include <cstring>
 #include <thread>
 #include <vector>
+#include <string>
+#include <unistd.h>
 
 #include "bitslice_gen.hpp"
+#include "bitslice_rule.hpp"
 #include "copy_pool.hpp"
 #include "dispatch.hpp"
 #include "gf256.hpp"
 #include "tile_order.hpp"
+#include "tune_table.hpp"
 
 using namespace callfs;
 
@@ -586,6 +592,58 @@ int main() {
     CHECK(bitslice_tile_order(128, false, false) == TileOrder::kGroup2);
     CHECK(bitslice_tile_order(512, false, false) == TileOrder::kSeg8);
     CHECK(bitslice_tile_order(512, true, true) == TileOrder::kXcd32);
+  }
+
+  // 9. the tune table
+  {
+    TuneTable t;
+    char path[] = "/tmp/callfs_tune_XXXXXX";
+    const int fd = mkstemp(path);
+    CHECK(fd >= 0);
+    if (fd >= 0) close(fd);
+    t.reset(path);
+    // keys: tiles per stripe bucketed by powers of two, alignment classes by addr_tz
+    const TuneKey a = tune_key(0, 10, 4, 128, 20, false, false, false, false);
+    CHECK(a.tps_log2 == 7 && a.align == 0 && a.kind == 0 && a.mis == 0);
+    CHECK(tune_key(0, 10, 4, 255, 20, false, false, false, false).packed() == a.packed());
+    CHECK(tune_key(0, 10, 4, 256, 20, false, false, false, false).packed() != a.packed());
+    CHECK(tune_key(0, 10, 4, 128, 10, false, false, false, false).align == 1);
+    CHECK(tune_key(0, 10, 4, 128, 4, true, false, true, false).packed() != a.packed());
+    CHECK(tune_key(1, 10, 4, 128, 20, false, false, false, false).packed() != a.packed());
+    CHECK(tune_key(0, 10, 4, 128, 20, true, true, false, true).kind == 2);
+    CHECK(tune_key(0, 10, 4, 128, 20, true, true, false, true).mis == 2);
+    CHECK(tune_key(0, 10, 4, 0, 20, false, false, false, false).tps_log2 == 0);
+    // empty: every lookup falls back to the rule (-1)
+    CHECK(t.empty() && t.lookup(a) == -1);
+    t.record(a, 98);
+    t.record(a, -1);  // no choice: ignored
+    CHECK(t.lookup(a) == 98 && t.size() == 1);
+    t.record(a, 258);  // a later tune replaces it
+    CHECK(t.lookup(a) == 258 && t.size() == 1);
+    const TuneKey b = tune_key(0, 32, 16, 8, 63, true, false, true, false);
+    t.record(b, 257);
+    CHECK(t.lookup(b) == 257 && t.lookup(a) == 258 && t.size() == 2);
+    // persistence: a new table bound to the same file reads both entries back
+    TuneTable u;
+    u.reset(path);
+    CHECK(u.size() == 2 && u.lookup(a) == 258 && u.lookup(b) == 257);
+    u.reset(nullptr);  // memory only (CALLFS_RS_TUNE_TABLE unset in this test)
+    CHECK(u.empty());
+    // concurrent tuners and launches
+    std::vector<std::thread> ths;
+    for (int w = 0; w < 4; ++w)
+      ths.emplace_back([&t, w] {
+        for (int i = 0; i < 200; ++i) {
+          const TuneKey k = tune_key(w, 4 + i % 20, 1 + i % 16, 1u << (i % 12), i % 24, i & 1,
+                                     false, i & 2, false);
+          t.record(k, i % 7);
+          (void)t.lookup(k);
+        }
+      });
+    for (auto& x : ths) x.join();
+    CHECK(t.size() > 2);
+    std::remove(path);
+    std::remove((std::string(path) + ".tmp").c_str());
   }
 
   std::printf(fails ? "FAILED %d\n" : "host_test ok\n", fails);

@@ -104,6 +104,7 @@ def test_plan_entry_points_refuse_null_plans(native_lib):
     assert L.rs_plan_tune(None, None, 1, None, 0) == E
     assert L.rs_plan_groups(None) == 0
     assert L.rs_plan_forms(None, orders, 2) == E
+    assert L.rs_tune_table_reset(None) == 0 and L.rs_tune_table_entries() == 0
 
 
 def test_init_fails_loudly_without_gpu(native_lib):

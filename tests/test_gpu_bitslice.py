@@ -14,6 +14,14 @@ pytestmark = pytest.mark.gpu
 BS_ORDERS = ["bs", "bs-g8", "bs-g2", "bs-q8", "bs-q16", "bs-x8", "bs-x32"]
 
 
+@pytest.fixture(autouse=True)
+def _no_tuned_forms(native_lib):
+    """The forms asserted below are the rule's: forget what other tests' tuners recorded."""
+    native_lib.lib.rs_tune_table_reset(None)
+    yield
+    native_lib.lib.rs_tune_table_reset(None)
+
+
 def _consistent(k, m, S, batch, seed, layout="planar"):
     """A resident batch whose parity the oracle computed (so every stripe is consistent),
     and its host copy [batch][n][S]."""
@@ -264,3 +272,40 @@ def test_host_codec_wide_profile_roundtrip(native_lib):
         lost[i] = None
     assert c.decode(lost, ErasureProfile(k, m), len(data)) == data
     assert S == -(-len(data) // k)
+
+
+def test_tune_table_serves_untuned_plans_and_persists(native_lib, tmp_path):
+    """Verdict r05 item 5: rs_plan_tune's choices land in a per-device table keyed by shape;
+    an untuned plan of the same shape (another size in the same tiles-per-stripe bucket) runs
+    the recorded form, bit-exact; CALLFS_RS_TUNE_TABLE's file keeps it for later processes;
+    a reset returns launches to the rule."""
+    from callfs_amd.device import Plan
+    L = native_lib.lib
+    path = str(tmp_path / "tune.txt")
+    assert L.rs_tune_table_reset(path.encode()) == 0
+    k, m, S = 32, 8, 262_144
+    sb, host = _consistent(k, m, S, 8, seed=11)
+    rule = Plan.for_batch(sb).forms()
+    # another shard size in the same key: 32..63 tiles of 8 KiB, shard pitch a multiple of
+    # 128 KiB (the planar layout's pitch is S here)
+    S2 = 3 * 131_072
+    sb2, host2 = _consistent(k, m, S2, 4, seed=12)
+    rule2 = Plan.for_batch(sb2).forms()
+    tuned = Plan.for_batch(sb)
+    chosen = tuned.tune(reps=2)
+    assert L.rs_tune_table_entries() >= 1
+    other = Plan.for_batch(sb2)
+    assert other.forms() == chosen, (rule, chosen)
+    for i in range(k, k + m):
+        sb2.zero_shard(i)
+    other.launch()
+    assert np.array_equal(sb2.gather().cpu().numpy(), host2), chosen
+    lines = open(path).read().split("\n")
+    assert any(ln.split()[1:3] == [str(k), str(m)] for ln in lines if ln.strip()), lines
+    # a fresh binding reads the file back; a reset to memory only forgets it
+    assert L.rs_tune_table_reset(path.encode()) == 0
+    assert L.rs_tune_table_entries() >= 1
+    assert Plan.for_batch(sb2).forms() == chosen
+    assert L.rs_tune_table_reset(None) == 0
+    assert L.rs_tune_table_entries() == 0
+    assert Plan.for_batch(sb2).forms() == rule2

@@ -1489,7 +1489,7 @@ def test_plan_ceiling_modes_then_relaunch(native_lib, k, m, S, batch, erase):
     """rs_plan_launch_ceiling (bench.py's live roofline denominators): the read-only mode
     leaves every byte as it was; the write-only mode may overwrite the written rows, and
     relaunching the plan restores them bit-exactly; bad arguments are refused, and the
-    A/B build's measurement modes (no-lookup, aligned-window probes) are RS_E_UNSUPPORTED
+    A/B build's measurement modes (no-lookup, aligned-window probes) are RS_E_ARG
     in the product library."""
     import ctypes
     import torch
