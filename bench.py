@@ -544,6 +544,9 @@ def main(argv=None):
             "decode_verify_rows": verify_rows,
             # per launch group, chosen by rs_plan_tune before the warmup (None: the rule)
             "tile_order": orders,
+            # the kernel form each launch group ran in the timed steps (rs_plan_forms: a tile
+            # order of the nibble-table kernels, or "bs-*" for the bit-sliced ones)
+            "forms": {"encode": enc.forms(), "decode": dec.forms()},
             "parallelism": (f"byte-column slices over {world} GPU(s), no collective" if S_obj
                             else f"stripes sharded over {world} GPU(s), no collective"),
         },

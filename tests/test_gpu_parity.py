@@ -1655,7 +1655,7 @@ def test_readall_layout_round_trip(native_lib, k, m, S, batch, how):
     (6, 3, 16 * 496 + 16 * 62 + 5, 4),
     (12, 4, 5_592_406 // 64, 2),
 ])
-@pytest.mark.parametrize("how", ["rule", "tune", "tri-x32", "tri-q8", "tri-g2", "realign-x32"])
+@pytest.mark.parametrize("how", ["rule", "tune", "tri-x32", "tri-q8", "tri-g2", "realign-x32", "bs-x32", "bs-g8"])
 def test_readall_decode_into_fresh_buffers(native_lib, k, m, S, batch, how):
     """The decode CallFS runs on an io.ReadAll body (bench.py --layout readall --decode-into
     fresh): survivors at odd offsets in the body, the erased shards rebuilt into buffers of
