@@ -36,7 +36,10 @@ uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
 }
 
 // gfx950 (or the device's own gfx name when one is current); CALLFS_OFFLOAD_ARCH overrides.
-std::string target_arch() {
+// Resolved on the thread that creates the kernel (kernel_for), never on the compile worker:
+// the worker makes no HIP call, so one still compiling at process exit cannot race the HIP
+// runtime's teardown.
+std::string device_arch() {
   if (const char* e = std::getenv("CALLFS_OFFLOAD_ARCH")) return e;
   int dev = -1;
   hipDeviceProp_t p;
@@ -47,6 +50,10 @@ std::string target_arch() {
     if (!a.empty()) return a;
   }
   return "gfx950";
+}
+std::string target_arch() {
+  static const std::string a = device_arch();  // once per process (one gfx target per box)
+  return a;
 }
 
 // On-disk cache of code objects: CALLFS_RS_JIT_CACHE (a directory; "0" turns it off), else
@@ -148,7 +155,8 @@ Mode mode() {
   return m;
 }
 
-Kernel::Kernel(int K, int R, const uint8_t* coef) : net_(build_network(K, R, coef)) {
+Kernel::Kernel(int K, int R, const uint8_t* coef)
+    : net_(build_network(K, R, coef)), arch_(target_arch()) {
   (void)R;
   opt_.prefetch = 0;   // auto at compile time (compile_locked)
   opt_.min_waves = 0;  // auto_waves at compile time
@@ -245,7 +253,7 @@ void Kernel::compile_locked(std::unique_lock<std::mutex>& lk) {
   GenOptions opt = opt_;
   lk.unlock();
   const auto t0 = std::chrono::steady_clock::now();
-  const std::string arch = target_arch();
+  const std::string arch = arch_;
   // two shards in flight; groups that run at 2 waves per SIMD anyway have the registers for
   // four (profiles/r06/params1: RS(32,16) 74.8 -> 75.3 %, RS(20,16) 256 KiB 74.8 -> 75.3 %)
   if (opt.prefetch <= 0) opt.prefetch = auto_waves(net.R, 2) <= 2 ? 4 : 2;

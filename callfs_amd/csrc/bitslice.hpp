@@ -52,6 +52,7 @@ class Kernel : public std::enable_shared_from_this<Kernel> {
   void compile_locked(std::unique_lock<std::mutex>& lk);
 
   Network net_;
+  std::string arch_;  // the gfx target the code object is compiled for
   GenOptions opt_;
   mutable std::mutex mu_;
   std::condition_variable cv_;

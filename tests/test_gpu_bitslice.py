@@ -4,6 +4,8 @@ case is bit-exact against the C oracle (oracle/rs_oracle.c via oracle.cref): enc
 wide profiles, 9..16-erasure decodes, Verify rows that pass on clean stripes and flag a
 flipped byte, ragged shard sizes (partial waves, a lane's second vector past the shard, the
 S % 16 byte tail), misaligned layouts, two launch groups, and every tile order pinned."""
+import os
+
 import numpy as np
 import pytest
 
@@ -309,3 +311,38 @@ def test_tune_table_serves_untuned_plans_and_persists(native_lib, tmp_path):
     assert L.rs_tune_table_reset(None) == 0
     assert L.rs_tune_table_entries() == 0
     assert Plan.for_batch(sb2).forms() == rule2
+
+
+def test_bitslice_off_runs_the_nibble_kernels(native_lib, tmp_path):
+    """CALLFS_RS_BITSLICE=0 (or a box where hiprtc cannot compile): every launch group runs
+    the ahead-of-time nibble-table kernels, bit-exact, and no bit-sliced order is offered."""
+    import subprocess
+    import sys
+    prog = tmp_path / "off.py"
+    prog.write_text(
+        "import sys, numpy as np\n"
+        f"sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})\n"
+        "import torch\n"
+        "from oracle import cref\n"
+        "from callfs_amd import _native as N\n"
+        "from callfs_amd.device import Plan, StripeBatch\n"
+        "k, m, S = 20, 16, 40_000 + 9\n"
+        "sb = StripeBatch(k, m, S, 2, torch.device('cuda:0'), layout='planar')\n"
+        "sb.fill_random(3)\n"
+        "p = Plan.for_batch(sb)\n"
+        "assert not p.forms()[0].startswith('bs'), p.forms()\n"
+        "try:\n"
+        "    p.set_orders(['bs'])\n"
+        "    raise SystemExit('bs offered')\n"
+        "except N.NativeError as e:\n"
+        "    assert e.code == N.RS_E_ARG\n"
+        "p.launch(); torch.cuda.synchronize()\n"
+        "h = sb.gather().cpu().numpy()\n"
+        "for b in range(2):\n"
+        "    want = cref.encode([h[b, i] for i in range(k)], k, m)\n"
+        "    assert all(np.array_equal(h[b, k + j], want[j]) for j in range(m))\n"
+        "print('off ok')\n")
+    env = dict(os.environ, CALLFS_RS_BITSLICE="0")
+    r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 0 and "off ok" in r.stdout, r.stdout + r.stderr[-2000:]
