@@ -38,7 +38,10 @@ inline TileOrder bitslice_tile_order(uint64_t tps, bool misaligned, bool verify)
   if (misaligned && verify) return TileOrder::kXcd32;
   if (tps <= 32) return TileOrder::kGroup8;
   if (tps <= 256) return TileOrder::kGroup2;
-  return TileOrder::kSeg8;
+  // above 2 MiB shards 16 column segments (profiles/r06/long1, % of 8 TB/s, Q8 -> Q16):
+  // RS(32,16) 4 MiB 70.4 -> 72.3, 16 MiB 71.6 -> 73.3, RS(20,16) 4 MiB 68.9 -> 71.3,
+  // RS(10,16) 4 MiB 70.2 -> 72.7, RS(32,8) 8 MiB 72.2 -> 73.1
+  return TileOrder::kSeg16;
 }
 
 }  // namespace callfs

@@ -718,7 +718,7 @@ std::vector<int> order_candidates(const ApplyArgs& a, bool every_instance) {
     add(TileOrder::kGroup2);
     if (tps <= 32 || every_instance) add(TileOrder::kGroup8);
     if (tps >= 64 || every_instance) add(TileOrder::kSeg8);
-    if (tps > 1024 || every_instance) add(TileOrder::kSeg16);
+    if (tps >= 256 || every_instance) add(TileOrder::kSeg16);
     if (every_instance) {
       add(TileOrder::kXcd8);
       add(TileOrder::kXcd32);

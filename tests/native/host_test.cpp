@@ -590,7 +590,8 @@ int main() {
     CHECK(!bitslice_rule(16, 8, 32, false, false, false, false));
     CHECK(bitslice_tile_order(8, false, false) == TileOrder::kGroup8);
     CHECK(bitslice_tile_order(128, false, false) == TileOrder::kGroup2);
-    CHECK(bitslice_tile_order(512, false, false) == TileOrder::kSeg8);
+    CHECK(bitslice_tile_order(512, false, false) == TileOrder::kSeg16);
+    CHECK(bitslice_tile_order(256, false, false) == TileOrder::kGroup2);
     CHECK(bitslice_tile_order(512, true, true) == TileOrder::kXcd32);
   }
 

@@ -346,3 +346,66 @@ def test_bitslice_off_runs_the_nibble_kernels(native_lib, tmp_path):
     r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, env=env,
                        timeout=300)
     assert r.returncode == 0 and "off ok" in r.stdout, r.stdout + r.stderr[-2000:]
+
+
+def test_host_memory_paths_with_bitslice_sync(native_lib, tmp_path):
+    """The host-memory entry points on wide profiles with CALLFS_RS_BITSLICE=sync (the first
+    call compiles and waits, so every launch group the rule gives the bit-sliced kernel runs
+    it): rs_codec_encode / rs_codec_decode through the staged pipeline (pageable buffers,
+    several chunks), rs_encode / rs_reconstruct on rs_host_alloc buffers (zero-copy: the
+    kernel reads host memory over PCIe), and rs_encode_batch / rs_reconstruct_batch; every
+    byte against the C oracle."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prog = tmp_path / "sync.py"
+    prog.write_text(
+        "import sys, numpy as np\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "import torch\n"
+        "from oracle import cref\n"
+        "from callfs_amd import Codec, ErasureProfile, erasure as E, _native as N\n"
+        "rng = np.random.default_rng(21)\n"
+        "c = Codec()\n"
+        "for k, m, L in ((20, 12, 40 * (1 << 20) + 13), (32, 16, 3 * (1 << 20) + 5), (24, 9, 777_777)):\n"
+        "    data = rng.integers(0, 256, L, dtype=np.uint8).tobytes()\n"
+        "    sh = c.encode(data, ErasureProfile(k, m))\n"
+        "    want = cref.encode([np.frombuffer(bytes(sh[i]), dtype=np.uint8) for i in range(k)], k, m)\n"
+        "    assert all(np.array_equal(np.frombuffer(bytes(sh[k + j]), dtype=np.uint8), want[j]) for j in range(m)), (k, m)\n"
+        "    lost = list(sh)\n"
+        "    for i in list(range(0, k, 3))[: m // 2] + list(range(k, k + m - m // 2)):\n"
+        "        lost[i] = None\n"
+        "    assert c.decode(lost, ErasureProfile(k, m), L) == data, (k, m)\n"
+        "# zero-copy: every buffer from rs_host_alloc\n"
+        "ctx = N.default_context()\n"
+        "k, m, S = 20, 16, 2 * (1 << 20) + 48\n"
+        "bufs = [N.PinnedBuffer(S, ctx) for _ in range(k + m)]\n"
+        "for i in range(k):\n"
+        "    bufs[i].array[:] = rng.integers(0, 256, S, dtype=np.uint8)\n"
+        "E.encode_shards([b.array for b in bufs], k, m, ctx)\n"
+        "want = cref.encode([bufs[i].array.copy() for i in range(k)], k, m)\n"
+        "assert all(np.array_equal(bufs[k + j].array, want[j]) for j in range(m))\n"
+        "keep = [b.array.copy() for b in bufs]\n"
+        "gone = [0, 1, 2, 3, 4, 5, 6, 7, 20, 21, 22, 23, 24, 25, 26, 27]\n"
+        "arrs = [b.array for b in bufs]\n"
+        "for i in gone:\n"
+        "    arrs[i][:] = 0\n"
+        "lens_shards = [None if i in gone else arrs[i] for i in range(k + m)]\n"
+        "E.reconstruct(lens_shards, k, m, ctx)\n"
+        "assert all(np.array_equal(np.frombuffer(bytes(lens_shards[i]), dtype=np.uint8), keep[i]) for i in gone)\n"
+        "# batch\n"
+        "st = [[rng.integers(0, 256, 65_536 + 7 * b, dtype=np.uint8).tobytes() for _ in range(20)] for b in range(5)]\n"
+        "par, status = E.encode_batch(st, 20, 12)\n"
+        "assert status == [0] * 5\n"
+        "for b in range(5):\n"
+        "    w = cref.encode([np.frombuffer(s, dtype=np.uint8) for s in st[b]], 20, 12)\n"
+        "    assert all(np.array_equal(np.frombuffer(bytes(par[b][j]), dtype=np.uint8), w[j]) for j in range(12)), b\n"
+        "full = [list(st[b]) + [bytes(p) for p in par[b]] for b in range(5)]\n"
+        "dmg = [[None if i in (0, 5, 9, 20, 21, 22, 23, 24, 25, 26) else s for i, s in enumerate(f)] for f in full]\n"
+        "assert E.reconstruct_batch(dmg, 20, 12) == [0] * 5\n"
+        "assert all(bytes(dmg[b][i]) == full[b][i] for b in range(5) for i in range(32))\n"
+        "print('sync ok')\n")
+    env = dict(os.environ, CALLFS_RS_BITSLICE="sync", CALLFS_RS_JIT_CACHE="0")
+    r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, env=env,
+                       timeout=600)
+    assert r.returncode == 0 and "sync ok" in r.stdout, r.stdout + r.stderr[-3000:]
