@@ -264,6 +264,15 @@ def _launch_ms(fn, stream, reps=20, warm_ms=30.0):
     return sum(a.elapsed_time(b) for a, b in ev) / reps
 
 
+def kernel_label(plan, k):
+    """The kernel a plan's (first) launch group ran: the bit-sliced one generated for its
+    coefficient block or the nibble-table / v_perm kernel."""
+    form = plan.forms()[0]
+    if form.startswith("bs"):
+        return f"rs_bs (bit-sliced, generated for the plan's coefficients; {form})"
+    return "rs_apply_lds" if k >= 4 else "rs_apply_vec"
+
+
 def plan_ceilings(enc, dec, stream):
     """Same-process traffic ceilings of the two plans (rs_plan_launch_ceiling, DESIGN.md
     §6.1): each plan's read streams alone and write streams alone on the production grid
@@ -562,7 +571,7 @@ def main(argv=None):
         "decode_ms_median_min": [round(dec_all[len(dec_all) // 2], 4), round(dec_all[0], 4)],
         "roofline": {
             "bound": "hbm",
-            "kernel": ("rs_apply_lds" if k >= 4 else "rs_apply_vec") + " (encode plan)",
+            "kernel": kernel_label(enc, k) + " (encode plan)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -576,7 +585,7 @@ def main(argv=None):
         },
         "roofline_decode": {
             "bound": "hbm",
-            "kernel": ("rs_apply_lds" if k >= 4 else "rs_apply_vec") + " (decode plan)",
+            "kernel": kernel_label(dec, k) + " (decode plan)",
             "achieved": round(dec_achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
