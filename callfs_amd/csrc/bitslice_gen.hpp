@@ -250,7 +250,7 @@ __device__ __forceinline__ void tr8(u32 (&d)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) if (!(i & 1)) { const u32 a = d[i], b = d[i + 1]; d[i] = sel(0x55555555u, a, b << 1); d[i + 1] = sel(0x55555555u, a >> 1, b); }
 }
-__device__ __forceinline__ void ld32(u32 (&x)[8], const unsigned char* p, u64 va, bool lb) {
+__device__ __forceinline__ void load_pair(u32 (&x)[8], const unsigned char* p, u64 va, bool lb) {
   const u32x4* q = reinterpret_cast<const u32x4*>(p);
   // no branch: a lane whose second vector lies past the shard reloads its first (the bit
   // planes keep byte positions apart, so those bytes only reach outputs it does not store)
@@ -301,13 +301,13 @@ __device__ __forceinline__ void map_tile(const Args& a, u32 b, u32& stripe, u32&
     for (int k = 0; k < 8; ++k) o += fmt("%s %s", k ? "," : "", acc(r, k).c_str());
     o += ";\n";
   }
-  for (int i = 0; i < D; ++i) o += fmt("  u32 ld%d[8]; ld32(ld%d, in[%d], va, lb);\n", i, i, i);
+  for (int i = 0; i < D; ++i) o += fmt("  u32 sh%d[8]; load_pair(sh%d, in[%d], va, lb);\n", i, i, i);
   for (int i = 0; i < n.K; ++i) {
     if (i + D < n.K)
-      o += fmt("  u32 ld%d[8]; ld32(ld%d, in[%d], va, lb);\n", i + D, i + D, i + D);
+      o += fmt("  u32 sh%d[8]; load_pair(sh%d, in[%d], va, lb);\n", i + D, i + D, i + D);
     o += "  asm volatile(\"\" ::: \"memory\");\n  __builtin_amdgcn_sched_barrier(0);\n  {\n";
-    o += fmt("    tr8(ld%d);\n", i);
-    for (int j = 0; j < 8; ++j) o += fmt("    const u32 p%d_%d = ld%d[%d];\n", i, j, i, j);
+    o += fmt("    tr8(sh%d);\n", i);
+    for (int j = 0; j < 8; ++j) o += fmt("    const u32 p%d_%d = sh%d[%d];\n", i, j, i, j);
     detail::emit_combos(o, 'L', i, n.lo_used[i], 0);
     detail::emit_combos(o, 'H', i, n.hi_used[i], 4);
     auto cname = [&](char P, int s, int plane0) {

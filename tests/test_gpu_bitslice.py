@@ -409,3 +409,28 @@ def test_host_memory_paths_with_bitslice_sync(native_lib, tmp_path):
     r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, env=env,
                        timeout=600)
     assert r.returncode == 0 and "sync ok" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("k,m", [(33, 9), (64, 16), (120, 12)])
+def test_more_than_32_inputs(native_lib, k, m):
+    """K > 32 (round 6's first generator named shard 32's buffer after its load helper, and
+    those kernels did not compile): encode and an m-erasure decode, rule and pinned, against
+    the oracle."""
+    from callfs_amd.device import Plan
+    S = 8192 * 2 + 16 * 9 + 3
+    n = k + m
+    sb, host = _consistent(k, m, S, 2, seed=k)
+    enc = Plan.for_batch(sb)
+    assert enc.forms()[0].startswith("bs"), enc.forms()
+    erase = list(range(1, k, k // (m // 2)))[: m // 2]
+    erase += list(range(k, k + m - len(erase)))
+    dec = Plan.for_batch(sb, present=[i not in erase for i in range(n)])
+    for name in ("rule", "bs-x32"):
+        for p, lost in ((enc, range(k, n)), (dec, erase)):
+            if name != "rule":
+                _pin(p, name)
+            for i in lost:
+                sb.zero_shard(i)
+            p.launch()
+            assert not p.corrupt(), (name, k)
+            assert np.array_equal(sb.gather().cpu().numpy(), host), (name, k, list(lost))
