@@ -23,3 +23,22 @@ def test_host_code_under_sanitizer(tmp_path, san):
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "host_test ok" in r.stdout
+
+
+def test_bitslice_kernels_compile_for_gfx950(tmp_path):
+    """The bit-sliced kernels' generated sources compile with hiprtc for gfx950 on the CPU
+    (no GPU): encode blocks of 9, 16 and 8 rows over 10 to 64 inputs, K > 32 included (a
+    generator that shadowed a helper with shard 32's buffer compiled nothing above 32), and
+    the occupancy search ends with at most 16 spilled VGPRs."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    exe = tmp_path / "bs_compile"
+    subprocess.run([hipcc, "-O1", "-std=c++17", "-x", "hip", "--offload-arch=gfx950", "-I", INC,
+                    os.path.join(ROOT, "tests", "native", "bs_compile.cpp"),
+                    os.path.join(INC, "bitslice.cpp"), "-lhiprtc", "-o", str(exe)],
+                   check=True, capture_output=True)
+    env = dict(os.environ, CALLFS_RS_JIT_CACHE="0", CALLFS_OFFLOAD_ARCH="gfx950")
+    r = subprocess.run([str(exe), "10,9", "20,16", "33,12", "64,8"], capture_output=True,
+                       text=True, env=env, timeout=600)
+    assert r.returncode == 0 and "bs_compile ok" in r.stdout, r.stdout + r.stderr[-2000:]
