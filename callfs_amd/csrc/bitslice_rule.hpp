@@ -25,17 +25,24 @@ namespace callfs {
 //    shards (G2), on two boxes: RS(32,4) 1 MiB 72.7 -> 74.7 / 72.4 -> 74.8, RS(24,4) 74.1 ->
 //    75.5 / 74.0 -> 75.6 (profiles/r06/sweep1, sweep2); RS(20,4) 3.4 MB and RS(16,4) 4 MiB
 //    lose 2-3 points.
+//  * every read-only launch (a download's Verify with nothing lost, codec.go:59, paid on every
+//    download): the bit-sliced form reads 32 B per lane per shard and compares in registers
+//    at 85-91 % of 8 TB/s where the nibble rule ran 77-88 (profiles/r06/readonly*, readall_ro:
+//    RS(10,4) 1 MiB 85.6 -> 89.6, RS(16,4) 83.7 -> 89.8, RS(12,8) 77.3 -> 89.8, RS(6,6) 81.8 ->
+//    91.4; io.ReadAll layout RS(10,8) 553,574 B 73.0 -> 90.5, RS(4,2) 1 MiB + 1 74.4 -> 88.7).
+//    Launches that write a row and compare the others keep the nibble kernels at R <= 4
+//    (RS(10,4) {5} 77.6 against 72.7).
 inline bool bitslice_rule(int K, int R, uint64_t tps, bool in_misaligned, bool out_misaligned,
                           bool verify, bool read_only) {
-  if (R > 8) return true;
-  if (read_only) return false;
+  if (R > 8 || read_only) return true;
   if (R <= 4) return K >= 24 && tps >= 64 && tps <= 128 && !verify && !in_misaligned && !out_misaligned;
   if (verify && in_misaligned && !out_misaligned) return true;
   if (K >= 20) return true;
   return K >= 16 && tps >= 64 && tps <= 256;
 }
-inline TileOrder bitslice_tile_order(uint64_t tps, bool misaligned, bool verify) {
+inline TileOrder bitslice_tile_order(uint64_t tps, bool misaligned, bool verify, bool read_only) {
   if (misaligned && verify) return TileOrder::kXcd32;
+  if (read_only) return TileOrder::kGroup8;  // within a point of the best order 64 KiB - 6.7 MB
   if (tps <= 32) return TileOrder::kGroup8;
   if (tps <= 256) return TileOrder::kGroup2;
   // above 2 MiB shards 16 column segments (profiles/r06/long1, % of 8 TB/s, Q8 -> Q16):

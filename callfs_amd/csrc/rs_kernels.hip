@@ -646,7 +646,8 @@ bool takes_bitslice(const ApplyArgs& a) {
 TileOrder bitslice_rule_order(const ApplyArgs& a) {
   const uint32_t rows = a.R >= 32 ? ~0u : (1u << a.R) - 1;
   return bitslice_tile_order((a.S / 16 + bs::kTileVecs - 1) / bs::kTileVecs,
-                             (a.in_misalign | a.out_misalign) != 0, (a.verify_mask & rows) != 0);
+                             (a.in_misalign | a.out_misalign) != 0, (a.verify_mask & rows) != 0,
+                             (a.verify_mask & rows) == rows);
 }
 // bs::Args::order of a TileOrder (-1: no generated form)
 int bitslice_order(TileOrder o) {

@@ -581,18 +581,22 @@ int main() {
     CHECK(!bitslice_rule(10, 8, 128, false, false, false, false));
     CHECK(bitslice_rule(10, 8, 68, true, false, true, false));
     CHECK(!bitslice_rule(10, 8, 68, true, true, true, false));
-    CHECK(!bitslice_rule(10, 8, 68, true, false, true, true));
+    CHECK(bitslice_rule(10, 8, 68, true, false, true, true));   // read-only: every R
+    CHECK(bitslice_rule(10, 4, 128, false, false, true, true));
+    CHECK(!bitslice_rule(10, 4, 128, false, false, true, false));  // mixed R <= 4: nibble
     CHECK(bitslice_rule(32, 4, 128, false, false, false, false));
     CHECK(!bitslice_rule(32, 4, 256, false, false, false, false));
     CHECK(!bitslice_rule(16, 4, 128, false, false, false, false));
     CHECK(!bitslice_rule(10, 4, 128, false, false, false, false));
     CHECK(bitslice_rule(16, 8, 128, false, false, false, false));
     CHECK(!bitslice_rule(16, 8, 32, false, false, false, false));
-    CHECK(bitslice_tile_order(8, false, false) == TileOrder::kGroup8);
-    CHECK(bitslice_tile_order(128, false, false) == TileOrder::kGroup2);
-    CHECK(bitslice_tile_order(512, false, false) == TileOrder::kSeg16);
-    CHECK(bitslice_tile_order(256, false, false) == TileOrder::kGroup2);
-    CHECK(bitslice_tile_order(512, true, true) == TileOrder::kXcd32);
+    CHECK(bitslice_tile_order(8, false, false, false) == TileOrder::kGroup8);
+    CHECK(bitslice_tile_order(128, false, false, false) == TileOrder::kGroup2);
+    CHECK(bitslice_tile_order(512, false, false, false) == TileOrder::kSeg16);
+    CHECK(bitslice_tile_order(256, false, false, false) == TileOrder::kGroup2);
+    CHECK(bitslice_tile_order(512, true, true, false) == TileOrder::kXcd32);
+    CHECK(bitslice_tile_order(512, false, true, true) == TileOrder::kGroup8);
+    CHECK(bitslice_tile_order(512, true, true, true) == TileOrder::kXcd32);
   }
 
   // 9. the tune table

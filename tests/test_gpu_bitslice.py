@@ -220,15 +220,15 @@ def test_tiny_and_ragged_shards(native_lib, k, m, S):
 
 
 def test_read_only_verify_pinned(native_lib):
-    """Nothing lost (a download's Verify): every row compared; the rule keeps the nibble
-    kernel for read-only launches of R <= 8 rows, the pinned bit-sliced form compares the same
-    bytes."""
+    """Nothing lost (a download's Verify): every row compared; the rule runs read-only
+    launches on the bit-sliced kernel (G8), the nibble kernel pinned compares the same bytes,
+    and a flipped byte is flagged in either."""
     from callfs_amd.device import Plan
     k, m, S = 20, 8, 65_536 + 17
     sb, host = _consistent(k, m, S, 3, seed=99)
     ver = Plan.for_batch(sb, present=[True] * (k + m))
-    assert not ver.forms()[0].startswith("bs"), ver.forms()
-    for name in ("rule", "bs", "bs-g8"):
+    assert ver.forms() == ["bs-g8"], ver.forms()
+    for name in ("rule", "bs", "x32", "consecutive"):
         if name != "rule":
             _pin(ver, name)
         ver.launch()
@@ -434,3 +434,28 @@ def test_more_than_32_inputs(native_lib, k, m):
             p.launch()
             assert not p.corrupt(), (name, k)
             assert np.array_equal(sb.gather().cpu().numpy(), host), (name, k, list(lost))
+
+
+@pytest.mark.parametrize("k,m,S,layout", [(10, 4, (1 << 20) + 1, "readall"), (4, 2, 65_536 + 7, "readall"),
+                                          (10, 4, 1 << 20, "planar"), (6, 6, 300_003, "planar")])
+def test_read_only_verify_rule_and_flags(native_lib, k, m, S, layout):
+    """Read-only launches of every row count take the bit-sliced kernel (X32 on misaligned
+    io.ReadAll bodies, G8 else): clean stripes pass, a flipped byte in a data shard or a
+    parity shard (vector part or byte tail) flags exactly its stripe."""
+    import torch
+    from callfs_amd.device import Plan, StripeBatch
+    n = k + m
+    sb = StripeBatch(k, m, S, 3, torch.device("cuda:0"), layout=layout)
+    sb.fill_random(S % 1000 + k)
+    Plan.for_batch(sb).launch()
+    ver = Plan.for_batch(sb, present=[True] * n)
+    assert ver.forms() == ["bs-x32" if (layout == "readall" and S % 16) else "bs-g8"], ver.forms()
+    ver.launch()
+    assert not ver.corrupt()
+    for b, i, pos in ((0, 0, 5), (2, n - 1, S - 1), (1, k, S // 2)):
+        sb.shard(b, i)[pos] ^= 0x10
+        ver.launch()
+        assert ver.corrupt_stripes() == [b], (b, i, pos)
+        sb.shard(b, i)[pos] ^= 0x10
+    ver.launch()
+    assert not ver.corrupt()

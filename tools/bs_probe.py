@@ -6,7 +6,8 @@ For each shape: one resident batch, the rule's plan and one plan per pinned bit-
 timed in rotated rounds. One JSON line per shape: % of 8 TB/s (algorithmic bytes / mean
 launch time) per variant.
 
-shape spec: k,m,S,stripes[,erase]   erase: '-' encode, or '+'-joined erased indices
+shape spec: k,m,S,stripes[,erase]   erase: '-' encode, 'none' (read-only Verify), or '+'-joined
+erased indices
 usage: python tools/bs_probe.py --shape 32,16,1048576,64 [--orders bs,bs-q8]
 """
 import argparse
@@ -67,8 +68,8 @@ def main():
         ref = sb.gather()
         present = None
         lost = list(range(k, n))
-        if erase != "-":
-            lost = sorted({int(x) for x in erase.split("+")})
+        if erase != "-":  # 'none': every shard present (a download's Verify, read-only)
+            lost = [] if erase == "none" else sorted({int(x) for x in erase.split("+")})
             present = [i not in lost for i in range(n)]
         fresh = None
         if a.fresh and present is not None:
