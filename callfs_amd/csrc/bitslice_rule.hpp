@@ -36,13 +36,21 @@ inline bool bitslice_rule(int K, int R, uint64_t tps, bool in_misaligned, bool o
                           bool verify, bool read_only) {
   if (R > 8 || read_only) return true;
   if (R <= 4) return K >= 24 && tps >= 64 && tps <= 128 && !verify && !in_misaligned && !out_misaligned;
-  if (verify && in_misaligned && !out_misaligned) return true;
+  // R 5..8 launches that compare rows (one-shard decodes: a row written, the rest compared)
+  // on aligned outputs, misaligned inputs or not (profiles/r06/mixed_r8, nibble rule ->
+  // bit-sliced: RS(10,8) 256 KiB {1} 69.1 -> 74.6, 64 KiB 67.9 -> 72.5, RS(12,6) 1 MiB {2}
+  // 71.8 -> 75.4, RS(10,8) 6.7 MB {1} 71.7 -> 73.6, RS(8,8) 8 MiB 76.7 -> 78.1; one cell
+  // equal, RS(10,8) 1 MiB {0,5} 74.0 / 73.9)
+  if (verify && !out_misaligned) return true;
   if (K >= 20) return true;
   return K >= 16 && tps >= 64 && tps <= 256;
 }
 inline TileOrder bitslice_tile_order(uint64_t tps, bool misaligned, bool verify, bool read_only) {
   if (misaligned && verify) return TileOrder::kXcd32;
   if (read_only) return TileOrder::kGroup8;  // within a point of the best order 64 KiB - 6.7 MB
+  // written + compared rows: X32 up to 256 KiB and above 2 MiB, G2 between (mixed_r8: 1 MiB
+  // G2 ahead of X32 by 0.7-4.3 on 4 of 5 cells; 64 KiB, 6.7 MB and 8 MiB X32 ahead by 0.4-5.6)
+  if (verify) return tps <= 32 || tps > 256 ? TileOrder::kXcd32 : TileOrder::kGroup2;
   if (tps <= 32) return TileOrder::kGroup8;
   if (tps <= 256) return TileOrder::kGroup2;
   // above 2 MiB shards 16 column segments (profiles/r06/long1, % of 8 TB/s, Q8 -> Q16):

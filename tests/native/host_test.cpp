@@ -580,7 +580,11 @@ int main() {
     CHECK(bitslice_rule(32, 8, 256, false, false, false, false));
     CHECK(!bitslice_rule(10, 8, 128, false, false, false, false));
     CHECK(bitslice_rule(10, 8, 68, true, false, true, false));
-    CHECK(!bitslice_rule(10, 8, 68, true, true, true, false));
+    CHECK(!bitslice_rule(10, 8, 68, true, true, true, false));  // misaligned outputs: nibble
+    CHECK(bitslice_rule(10, 8, 128, false, false, true, false));  // aligned mixed R 5..8
+    CHECK(bitslice_tile_order(128, false, true, false) == TileOrder::kGroup2);
+    CHECK(bitslice_tile_order(8, false, true, false) == TileOrder::kXcd32);
+    CHECK(bitslice_tile_order(820, false, true, false) == TileOrder::kXcd32);
     CHECK(bitslice_rule(10, 8, 68, true, false, true, true));   // read-only: every R
     CHECK(bitslice_rule(10, 4, 128, false, false, true, true));
     CHECK(!bitslice_rule(10, 4, 128, false, false, true, false));  // mixed R <= 4: nibble
