@@ -24,6 +24,8 @@
 #include <string>
 #include <vector>
 
+#include <unistd.h>
+
 namespace callfs {
 
 struct TuneKey {
@@ -122,7 +124,8 @@ class TuneTable {
   }
   void save_locked() {
     if (path_.empty()) return;
-    const std::string tmp = path_ + ".tmp";
+    // one temp file per process: processes sharing a table file never write the same temp
+    const std::string tmp = path_ + "." + std::to_string(static_cast<long>(getpid())) + ".tmp";
     FILE* f = std::fopen(tmp.c_str(), "w");
     if (!f) return;
     bool ok = true;
@@ -132,7 +135,7 @@ class TuneTable {
                          k.kind, k.mis, kv.second.order) > 0;
     }
     ok &= std::fclose(f) == 0;
-    if (ok) (void)std::rename(tmp.c_str(), path_.c_str());
+    if (!ok || std::rename(tmp.c_str(), path_.c_str()) != 0) (void)std::remove(tmp.c_str());
   }
 
   std::mutex mu_;
