@@ -894,7 +894,7 @@ void rs_apply_lds(ApplyArgs a) {
       for (int j = 0; j < 4; ++j) acc[w][j] = lds_zero<RT>();
     // Verify rows' stored vectors, loaded VPF shards before the end of the input loop:
     // a compare load issued after the loop leaves each wave a full memory latency with
-    // nothing to do (tools/verify_prefetch_probe.sh: one write + three compare rows 71.6
+    // nothing to do (profiles/r02/verify_prefetch/: one write + three compare rows 71.6
     // -> 74.1 %, four compare rows 78.0 -> 80.9 %)
     constexpr bool kVpf = P::VPF > 0 && RT <= 4;
     uint4 vpre[kVpf ? RT : 1];
@@ -1196,7 +1196,7 @@ void rs_apply_lds(ApplyArgs a) {
       if (P::REALIGN && !active) continue;
       if ((a.verify_mask >> r) & 1u) {
         // non-temporal like the input loads: the all-Verify decode (every download,
-        // codec.go:59) ran 76.3-77.9 -> 79.7-80.2 % with them (tools/verify_nt_probe.sh)
+        // codec.go:59) ran 76.3-77.9 -> 79.7-80.2 % with them (round-2 probe, profiles/notebook_r01_r04.md)
         uint4 y;
         if constexpr (kVpf) y = vpre[r];
         else y = load16<P>(dst);
@@ -1331,8 +1331,8 @@ __global__ __launch_bounds__(kBlock) void rs_apply_bytes(ApplyArgs a, uint64_t b
 
 // ---- one-dispatch small calls (rs_kernels.hpp SmallArgs) -------------------------------
 // A host-memory call of a few KiB spent ~29 us in an H2D blit, the kernel and a D2H blit,
-// each a dispatch that waits for the previous one (tools/small_trace.sh: 6.6 + 7.6 + 4.2 us
-// on the GPU plus ~20 us on the host, profiles/r03/small_trace). This kernel reads the
+// each a dispatch that waits for the previous one (6.6 + 7.6 + 4.2 us on the GPU plus ~20 us
+// on the host, profiles/r03/small_path/r03_smalltrace2). This kernel reads the
 // lane's host-coherent staging buffer over PCIe and writes the outputs back into it: one
 // dispatch per call. Each lane owns one 16-B column vector of one stripe, so a call waits
 // for few PCIe round trips; the GF multiply is the v_perm form (tables in SGPRs, no LDS prologue).
@@ -1410,8 +1410,8 @@ __device__ __forceinline__ void small_vector(const SmallArgs& a, uint32_t v) {
 
 // The completion flag (SmallArgs::done): the host spins on it instead of waiting for the
 // runtime's completion signal, which returned ~5 us after the kernel had ended
-// (tools/small_trace.sh). Every thread makes its own stores visible system-wide (a
-// system-scope release per wave: the workgroup-scope release in __syncthreads does not wait
+// (profiles/r03/small_path/r03_smalltrace2). Every thread makes its own stores visible
+// system-wide (a system-scope release per wave: the workgroup-scope release in __syncthreads does not wait
 // for another wave's PCIe stores), then the block counts itself done on a device-memory
 // counter; the last block resets the counter and releases the call's sequence number into
 // the host flag.

@@ -1702,7 +1702,7 @@ int rs_plan_launch_ceiling_timed(rs_plan* plan, void* stream, int mode, void* st
 // candidate gets `reps` back-to-back launches between two events, in three rounds with the
 // candidate order rotated; the per-launch mean of the best round counts, and the rule's
 // order is kept unless another is faster by more than 1 % (with 0.3 % the tuner sometimes
-// left the rule for an order that then timed 0.5-1 % slower: tools/tune_small.sh).
+// left the rule for an order that then timed 0.5-1 % slower, round 3).
 namespace {
 constexpr int kTuneRounds = 3;
 constexpr float kTuneWarmMs = 150.0f;

@@ -51,7 +51,7 @@ using LdsPolicy = dev::Policy<2, 1, true, true, false, 512, 2, 0>;
 // base) instead of v_perm_b32: same issue rate (tools/valu_rates.hip, 0.24 per SIMD
 // clock), but no VGPR for the table base, which keeps R = 16 at 125 VGPRs (4 waves per
 // SIMD; the v_perm form had grown to 129 = 3 waves once the ragged tail moved into the
-// kernel). tools/sdwa_sweep.sh, profiles/r02/sdwa/, % of 8 TB/s, v_perm -> SDWA:
+// kernel). profiles/r02/sdwa/, % of 8 TB/s, v_perm -> SDWA:
 // RS(10,16) 58.3 -> 66.8, RS(20,16) 52.2 -> 59.3, RS(32,16) 49.0 -> 55.0, RS(10,12)
 // 65.9 -> 66.5.
 using LdsWidePolicy = dev::Policy<2, 1, true, true, false, 512, 4, 0, 1, false, false, true>;
@@ -65,7 +65,7 @@ using LdsQ16Policy = dev::Policy<2, 1, true, true, false, 512, 2, 8>;
 using LdsX8Policy = dev::Policy<2, 1, true, true, false, 512, 2, 10>;
 using LdsX32Policy = dev::Policy<2, 1, true, true, false, 512, 2, 11>;
 // Launch groups of R <= 4 rows with Verify rows load the compared vectors 4 shards before
-// the end of the input loop (rs_apply.hpp Policy::VPF): tools/verify_prefetch_probe.sh,
+// the end of the input loop (rs_apply.hpp Policy::VPF):
 // profiles/r02/verify_prefetch/, RS(10,4) 1 MiB x 256, % of 8 TB/s, after the loop ->
 // prefetch distance 2 / 4 / 6 / 8: one write + three compare rows 71.6 -> 72.7 / 74.1 /
 // 73.7 / 73.3, four compare rows 78.0 -> 79.3 / 80.9 / 80.8 / 79.5. Without Verify rows
@@ -78,7 +78,7 @@ using LdsVerifyPolicy = dev::Policy<2, 1, true, true, false, 512, 2, ORD, 0, fal
 // addresses realigned the same way (62 vectors per wave; the bytes no aligned block
 // covers are written by each stripe's first tile; rs_apply.hpp REALIGN 2). Round 1's
 // form realigned only the loads (REALIGN 1, 63 vectors per wave, k >= 8; kept in
-// tools/kbench for comparison). tools/realign_out_sweep.sh (round 2), tools/wave_tiling_probe.sh,
+// tools/kbench for comparison). Round 2,
 // profiles/r02/realign_out/, % of 8 TB/s, unaligned -> loads realigned -> loads and stores
 // realigned: RS(10,4) 64 MiB objects (S = 6,710,887) 67.6 -> 68.1 -> 69.5, RS(10,8)
 // 1,048,577 B 63.9 -> 65.3 -> 67.0, RS(6,3) 65.6 -> 67.0 -> 71.5, RS(5,3) 68.7 -> 66.7
@@ -152,7 +152,7 @@ int tile_order_override() {
 // spread over more of the address space than the tile order intends. Grids of more than
 // twice about 4 GiB of shard traffic are cut into equal consecutive slices of at most
 // that much (one launch each, same tile order), which resets the drift. Round 2 sweep
-// (tools/slice_rule_sweep.sh, profiles/r02/slice_rule/, % of 8 TB/s, unsliced / 2 GiB /
+// (profiles/r02/slice_rule/, % of 8 TB/s, unsliced / 2 GiB /
 // 4 GiB slices): RS(10,4) 64 MiB objects x 256 (24 GiB) 73.1 / 77.5 / 77.4, 1 MiB x 1,024
 // 77.9 / 79.2 / 79.4, RS(4,2) 1 MiB x 2,048 76.8 / 79.2 / 79.3: long memory-bound grids
 // need slices, and 4 GiB ones keep the gain. Every slice boundary drains the machine,
@@ -283,7 +283,7 @@ const std::array<std::array<VecFn, 8>, 6> kLdsTri = {
 // (rs_apply.hpp Policy::WIX 3): the compiler's waits then leave six loads in flight where
 // the rotating form waited for the next triple inside each iteration. 81 VGPRs (5 waves
 // per SIMD) at R <= 4; at R = 8 it needs 131 and lost (3 waves). Launches with R <= 4 and
-// K >= 6 that take the triple form run it. tools/tridb_probe.sh, profiles/r04/tridb/,
+// K >= 6 that take the triple form run it. profiles/r04/tridb/,
 // % of 8 TB/s, rotating -> double-buffered triples in the same order: RS(10,4) 1 MiB 76.6
 // -> 80.0 (G2), RS(8,4) 2 MiB 77.4 -> 80.5 (X32), RS(12,4) 1 MiB 79.4 -> 80.9 (G2),
 // RS(6,3) 1 MiB 75.6 -> 78.4, 4 MiB 75.8 -> 78.1 (X32), RS(6,3) 174,763 B 72.2 -> 75.9,
@@ -324,7 +324,7 @@ constexpr int kTriDbMinK = 6;
 // stripes of at most kTailLastMaxTps tiles whose last tile leaves that wave idle, else wave
 // 0 of the first tile. Round 4 moved every tail to the last tile (1 MiB-object shards, 7-22
 // tiles per stripe, gained 0.4-1.3 points); on long stripes that put the grid's last tile
-// behind the tail's load chain (tools/tail_ab.sh, profiles/r04/tail_ab: RS(20,4) S =
+// behind the tail's load chain (profiles/r04/tail_ab: RS(20,4) S =
 // 3,355,444, 410 tiles, first tile 73.8 %, last tile 72.6). CALLFS_RS_TAIL_LAST_TPS
 // overrides the bound (A/B build only; clamped so that (tps - 1) << 2 fits the 32-bit code).
 // Every LDS policy that takes this code tiles as LdsPolicy does (static_assert in

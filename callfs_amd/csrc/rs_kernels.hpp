@@ -81,7 +81,7 @@ struct SmallArgs {
   // device memory, uploaded once per (lane, tables): [K][R][5] v_perm tables of the group,
   // then idx: the shard index of input i (idx[i], the k valid shards) and of row r
   // (idx[256 + r]). Kept out of the kernel arguments: 272 B of arguments cost the launch
-  // ~2 us (tools/small_trace.sh)
+  // ~2 us (profiles/r03/small_path/r03_smalltrace2)
   const uint32_t* tabs;
   const uint8_t* idx;
   // idx[0..15] and idx[256..271] again, as kernel arguments: the data loads of a k <= 16

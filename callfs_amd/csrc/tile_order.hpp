@@ -71,7 +71,7 @@ enum class TileOrder { kConsecutive, kGroup8, kGroup2, kSeg8, kSeg16, kXcd8, kXc
 constexpr int kTileOrders = 7;
 
 
-// Tile order for R <= 8 (Policy::ORD; tools/kbench.hip KB_ORD, tools/order_sweep.sh,
+// Tile order for R <= 8 (Policy::ORD; tools/kbench.hip KB_ORD, profiles/r01/tile_order/,
 // 5-15 rounds, % of 8 TB/s, DESIGN.md "Tile order"). Neighbouring blocks normally take
 // neighbouring column tiles of one stripe (consecutive). For small shards it pays to
 // interleave the same column tile of G stripes instead: G8 up to 256 KiB (RS(10,4)
@@ -166,7 +166,7 @@ inline TileOrder tri_order(TileOrder nibble) {
 //  * round 3 (profiles/r03/r03s5, r03s6): launches that write every row or compare every
 //    row, shards up to 2 MiB (4 MiB with K <= 6), at <= 256 KiB only K <= 6 or R >= 5, in
 //    the nibble rule's order (G8 -> X32): RS(4,2) 1 MiB 72 -> 80.6, RS(10,8) 74.4 -> 78.2;
-//  * round 4, rotating form (tools/tri_sweep.sh, profiles/r04/tri_sweep1, tri_sweep2,
+//  * round 4, rotating form (profiles/r04/tri_sweep1, tri_sweep2,
 //    tri_validate, triord): K <= 5 in X32 up to 8 MiB and X8 above (RS(4,2) 8 MiB 70.0 ->
 //    79.6, 16 MiB 69.9 -> 81.1, 32 MiB 69.8 -> 81.4); R 5..8 with K = 6 in X32 / Q16;
 //    read-only launches in X32 at every size (RS(6,3) 16 MiB 85.7 -> 90.0, RS(10,4) 4 MiB
@@ -242,7 +242,7 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     // and the ring in consecutive order above (RS(16,4) 8 of 9 sizes, 832,781 B 69.2 -> 74.3)
     if (tps <= 128) return addr_tz >= 17 ? g2 : K > 12 ? -1 : x32;
     // K >= 10 on 1-8 MiB shards at pitches that are not a power of two: the ring of three in
-    // consecutive order (round 4, fourth session, tools/mid_shard_probe.sh,
+    // consecutive order (round 4, fourth session,
     // profiles/r04/mid1/, two passes, one-block layout, tri-Q8 -> ring: RS(10,4) 1.68 MB
     // 74.2 -> 75.2, 6.7 MB 73.2 -> 74.0, RS(12,4) 1.4 MB 73.2 -> 75.2, 5.6 MB 71.4 -> 74.9;
     // power-of-two pitches keep tri-Q8: RS(8,4) 2 MiB 77.2 vs 75.0, 4 MiB 74.9 vs 72.2)
@@ -279,7 +279,7 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     if (K >= 10 && tps > 256) return q8;
   }
   // R 5..8 on shards up to 256 KiB: the rotating triples in X32 for any K (round 4,
-  // planar 1 MiB objects, tools/small_r8_probe.sh, profiles/r04/smallr8/ab.jsonl: RS(32,8)
+  // planar 1 MiB objects, profiles/r04/smallr8/ab.jsonl: RS(32,8)
   // 32 KiB 65.9 -> 69.3, one-block layout 66.9 -> 68.7; RS(16,8) 64 KiB 69.8 -> 73.2)
   // (round 5, planar: G2 for K <= 12 where the pitch is a multiple of 128 KiB, RS(8,8) 128 KiB
   // X32 75.4 / 75.5 -> G2 76.3 / 76.5; elsewhere X32, which leads G2 on 23 of 30 sizes from
@@ -289,7 +289,7 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
   if (K > 12) return -1;
   if (tps <= 32) return K <= 6 || R >= 5 ? x32 : -1;
   if (read_only) return x32;
-  // K <= 5 above 8 MiB: X8 (tools/triord_probe.sh, profiles/r04/triord/: RS(4,2) 16 MiB
+  // K <= 5 above 8 MiB: X8 (profiles/r04/triord/: RS(4,2) 16 MiB
   // 71.7 -> 81.1, 32 MiB 77.5 -> 81.4, 16 MiB at a padded pitch 76.6 -> 80.4; 8 MiB X32
   // 80.9 vs X8 79.4)
   if (K <= 5) return tps > 1024 ? x8 : x32;
@@ -323,7 +323,7 @@ inline bool tri_tunable(int K, int R, bool misaligned, bool verify, bool read_on
   return R <= 8 && K >= 3 && (K <= 16 || R <= 4) && !misaligned && (!verify || read_only || R <= 4);
 }
 // Wide groups hold 19-32 shard streams per stripe; from 2 MiB shards on, 8 interleaved
-// column segments beat consecutive tiles (tools/order_sweep.sh, KB_ORD, 9 rounds, % of
+// column segments beat consecutive tiles (tools/kbench.hip KB_ORD, 9 rounds, % of
 // 8 TB/s: RS(10,12) 4 MiB 60.3 -> 66.9, RS(10,16) 16 MiB 58.0 -> 66.7; at 1 MiB all
 // orders are within 0.6 of each other, profiles/r01/tile_order/segments/ord_wide).
 inline TileOrder wide_tile_order(uint64_t tps) {
@@ -331,7 +331,7 @@ inline TileOrder wide_tile_order(uint64_t tps) {
 }
 
 // Tile order of the v_perm kernel (k <= 3: at most 7 shard streams per stripe;
-// tools/order_sweep.sh KB_ORD "vperm ord", 7 rounds, % of 8 TB/s,
+// tools/kbench.hip KB_ORD "vperm ord", 7 rounds, % of 8 TB/s,
 // profiles/r01/tile_order/segments/ord_vperm): 2-stripe interleave up to 8 MiB shards
 // (RS(3,2) 1 MiB 74.9 -> 77.6, 5.6 MB 75.6 -> 80.6, RS(2,1) 64 KiB 74.9 -> 78.2, RS(2,2)
 // 4 MiB 75.9 -> 77.6; RS(1,1) 1 MiB 79.2 -> 78.4), 16 column segments above 8 MiB when
