@@ -237,7 +237,7 @@ std::vector<char> rtc_compile(const std::string& src, const std::vector<std::str
 
 // Waves per SIMD to ask for: the VGPRs a group needs are about 8 accumulator planes per row,
 // 8 per input shard in flight and ~40 for the planes and combos of the shard being consumed
-// and addresses; 512 VGPRs per SIMD lane (tools/bs_params_r06.sh, profiles/r06/params1: R = 8
+// and addresses; 512 VGPRs per SIMD lane (tools/jobs.sh bs_params_r06, profiles/r06/params1: R = 8
 // at 4 waves 75.9 -> 79.1 % for RS(32,8) 2 MiB; R = 16 forced to 3 waves spilled ~1,000 VGPRs
 // and ran at 12 %).
 int auto_waves(int R, int prefetch) {

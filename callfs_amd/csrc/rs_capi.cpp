@@ -908,7 +908,7 @@ int run_host_impl(rs_ctx* ctx, Lane& L, int device, const std::shared_ptr<const 
   // (tests/perf/zerocopy_probe.py).
   // Threshold: 48 KiB per shard over the call (S x batch), i.e. 48 KiB x n over all n
   // shards. Below it the one-dispatch path on the library's coherent staging is faster;
-  // tools/zc_threshold.sh (profiles/r04/zc_threshold/zc.jsonl, GiB/s enc / dec, 1 thread,
+  // tools/jobs.sh zc_threshold (profiles/r04/zc_threshold/zc.jsonl, GiB/s enc / dec, 1 thread,
   // zero-copy vs one-dispatch): RS(4,2) 128 KiB objects 4.6 / 4.2 vs 6.2 / 5.9, 256 KiB
   // 8.7 / 7.7 vs 5.3 / 5.3; RS(10,4) 384 KiB 9.6 / 8.9 vs 9.0 / 9.1, 512 KiB 11.7 / 11.4 vs
   // 8.0 / 10.0; RS(16,4) 512 KiB 11.2 / 9.1 vs 10.9 / 9.2, 1 MiB 20.9 / 17.1 vs 10.8 / 14.6.

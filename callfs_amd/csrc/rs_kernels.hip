@@ -552,7 +552,7 @@ int tri_unaligned_order(const ApplyArgs& a, uint64_t tps) {
   // RS(10,8) {1}, 122 KB - 24 MB: 62-64 vs 65.7-71.0; after: those 8 cells 63.7 -> 66.4
   // on average, random_readall_dec1_after.jsonl)
   if (a.R > 4 && verify) return -1;
-  // round 5 (tools/readall_rule_sweep.sh, profiles/r05/readall_rule/): Q8 from 1 to 2 MiB,
+  // round 5 (tools/jobs.sh readall_rule_sweep, profiles/r05/readall_rule/): Q8 from 1 to 2 MiB,
   // X32 -> Q8: RS(10,4) 1.68 MB 74.9 -> 76.6, RS(12,4) 1.4 MB 75.1 -> 76.3, RS(8,8) 2 MiB
   // 75.0 -> 76.3, RS(10,8) 1.68 MB 70.4 -> 71.7
   if (tps > 128 && tps <= 256) return static_cast<int>(TileOrder::kSeg8);

@@ -130,7 +130,7 @@ inline TileOrder lds_tile_order(uint64_t S, uint64_t tps, int addr_tz, int strea
   // exactly 1 MiB apart: G2 beats G8 (RS(4,4) 128 KiB 61.2 -> 68.7, RS(8,8) 64 KiB 64.2
   // -> 67.7, RS(12,4) 64 KiB equal)
   if (stripe_stride == (1ull << 20) && tps <= 32) return TileOrder::kGroup2;
-  // round 5, planar layout (tools/rule_sweep.sh, profiles/r05/rule/): more than 16 inputs
+  // round 5, planar layout (tools/jobs.sh rule_sweep, profiles/r05/rule/): more than 16 inputs
   // with R <= 4 on 256 KiB - 1 MiB shards run the ring faster in consecutive order
   // (RS(20,4) 838,861 B G2 73.9 / 73.4 -> consecutive 74.9 / 74.7); the same from 13 inputs
   // and down to the smallest shards, where tri_rule_order leaves these launches to the ring
@@ -202,7 +202,7 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     if (R > 4) return -1;
     if (K <= 4) return x32;
     if (db) {  // round 4 (profiles/r04/tri_verify_ab2): G2 up to 1 MiB, X32 above
-      // round 5, planar (tools/decode_rule_sweep.sh, profiles/r05/decode_rule/): up to 256 KiB
+      // round 5, planar (tools/jobs.sh decode_rule_sweep, profiles/r05/decode_rule/): up to 256 KiB
       // the early-compare triples for K >= 7, where the ring ran (in G2: RS(10,4) 104,858 B
       // erase {1} 71.0 -> 75.7, {10} 72.0 -> 76.9; RS(12,4) 87,382 B {1} 69.3 -> 75.2; RS(8,4)
       // 128 KiB {1} 74.6 -> 77.6; RS(16,4) 64 KiB {1} 70.5 -> 77.3)
@@ -246,7 +246,7 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     // profiles/r04/mid1/, two passes, one-block layout, tri-Q8 -> ring: RS(10,4) 1.68 MB
     // 74.2 -> 75.2, 6.7 MB 73.2 -> 74.0, RS(12,4) 1.4 MB 73.2 -> 75.2, 5.6 MB 71.4 -> 74.9;
     // power-of-two pitches keep tri-Q8: RS(8,4) 2 MiB 77.2 vs 75.0, 4 MiB 74.9 vs 72.2)
-    // round 5, planar (tools/rule_sweep.sh, tools/cfg12_orders.sh, profiles/r05/): above 1 MiB
+    // round 5, planar (tools/jobs.sh rule_sweep, tools/jobs.sh cfg12_orders, profiles/r05/): above 1 MiB
     // the ring in consecutive order for K >= 10 at every pitch (RS(10,4) 2 MiB tri-Q8 72.9 ->
     // ring 76.9, 4 MiB 74.8 -> 75.4, 8 MiB 72.6 -> 75.6; round 4 kept tri-Q8 on power-of-two
     // pitches in the one-block layout), except Q16 on 16-32 MiB power-of-two pitches (round 4,
@@ -263,7 +263,7 @@ inline int tri_rule_order(int K, int R, bool misaligned, bool verify, bool read_
     return pow2_16_32 ? q16 : -1;
   }
   // Read-only launches (every row compared: the download with nothing lost), round 5, planar
-  // (tools/decode_rule_sweep.sh, profiles/r05/decode_rule/): R 5..8 keep the ring, which
+  // (tools/jobs.sh decode_rule_sweep, profiles/r05/decode_rule/): R 5..8 keep the ring, which
   // runs 5-7 points ahead of the rotating triples there (RS(10,8) 104,858 B tri-X32 71.6 ->
   // ring 76.5, 1.68 MB 71.1 -> 78.3, 6.7 MB 72.1 -> 78.1); R <= 4 take the triples up to 256
   // KiB in consecutive order (RS(16,4) 64 KiB ring 78.3 -> 83.7, RS(12,4) 87,382 B 78.2 ->

@@ -34,7 +34,7 @@ var (
 	gpuCtx  *C.rs_ctx // nil: no usable device, every call takes the CPU codec
 	// CALLFS_ERASURE__GPU_MIN_BYTES: objects below this stay on the CPU codec
 	// (INTEGRATION.md "when the GPU pays"). 64 MiB is where one GPU call passes one CPU
-	// thread on the round-6 build (DESIGN.md §7.4 "CPU or GPU", tools/n1_r06.sh,
+	// thread on the round-6 build (DESIGN.md §7.4 "CPU or GPU", tools/jobs.sh n1_r06,
 	// profiles/r06/n1/): RS(10,4) 28.2 vs 20.0 GiB/s from pageable buffers and 33.0 through
 	// pinned bodies (BodyBuffer), RS(4,2) 34.7 vs 29.3 through pinned bodies; at 16 MiB the
 	// cache-resident CPU port leads (51-53 vs 20-33); one threshold for every profile.

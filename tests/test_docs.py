@@ -64,12 +64,16 @@ def test_design_citations_name_existing_sections():
 
 
 TOOL = re.compile(r"\btools/([A-Za-z0-9_]+\.(?:sh|py|hip|cpp|h|txt))")
+JOB = re.compile(r"\btools/jobs\.sh ([a-z0-9_]+)")
 
 
 def test_cited_tools_exist():
     """Current docs and sources cite only tools that exist (verdict r05 item 6: comments
     citing deleted probes). profiles/README.md and the rounds 1-4 notebook index data whose
     one-shot probes were retired; they say so and are not checked."""
+    jobs = set(re.findall(r"^job_([a-z0-9_]+)\(\) \{$",
+                          open(os.path.join(ROOT, "tools", "jobs.sh")).read(), flags=re.M))
+    assert {"gpu_tests", "gpu_round", "profile", "n1_r06"} <= jobs, sorted(jobs)
     bad = []
     for f in cited_files():
         if os.path.relpath(f, ROOT) == os.path.join("profiles", "README.md"):
@@ -82,6 +86,10 @@ def test_cited_tools_exist():
             if not os.path.exists(os.path.join(ROOT, "tools", m.group(1))):
                 line = text.count("\n", 0, m.start()) + 1
                 bad.append(f"{os.path.relpath(f, ROOT)}:{line}: tools/{m.group(1)}")
+        for m in JOB.finditer(text):
+            if m.group(1) not in jobs:
+                line = text.count("\n", 0, m.start()) + 1
+                bad.append(f"{os.path.relpath(f, ROOT)}:{line}: no job {m.group(1)} in tools/jobs.sh")
     assert not bad, "\n".join(bad)
 
 

@@ -54,7 +54,7 @@ def test_planar_layout_separates_data_and_parity():
 
 @pytest.mark.parametrize("layout", ["planar", "pitch", "shardmajor"])
 def test_explicit_pitch(layout):
-    """StripeBatch(pitch=P) (bench.py --pitch, tools/pitch_sweep.sh): every shard at that
+    """StripeBatch(pitch=P) (bench.py --pitch, tools/jobs.sh pitch_sweep): every shard at that
     pitch within its region; a pitch below S, not a multiple of 16, or for an upstream Split
     layout is refused."""
     k, m, S, P = 10, 4, 6_710_887 // 64, 6_710_887 // 64 + 4096 + 9

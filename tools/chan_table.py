@@ -1,4 +1,4 @@
-"""Table of tools/chan_probe.sh's memory-side counters (development tool).
+"""Table of tools/jobs.sh chan_probe's memory-side counters (development tool).
 
 Per shape (in --shape order) and variant (the plan's launch, its read streams alone, its
 write streams alone): µs per launch under the profiler, average read / write latency in

@@ -1,5 +1,5 @@
 """Launch one plan N times in a given order (development tool: the program rocprofv3 profiles
-for PMC passes, tools/pmc_forms.sh). shape spec as tools/ceiling_sweep.py.
+for PMC passes, tools/jobs.sh pmc_forms). shape spec as tools/ceiling_sweep.py.
 usage: python tools/plan_run.py --shape 10,8,6710887,32,-,planar --order tri-q8 --launches 20"""
 import argparse
 import os

@@ -1,4 +1,4 @@
-"""Table of tools/pmc_bs.sh: per kernel form of one shape, % of 8 TB/s (kernel trace), clock,
+"""Table of tools/jobs.sh pmc_bs: per kernel form of one shape, % of 8 TB/s (kernel trace), clock,
 VALU instructions per input byte, VALU issue share, LDS issue share, waves per SIMD, wait
 share and instruction-cache misses (development tool).
 usage: python tools/pmc_bs_table.py <gpurun_out/tag> <k> <m> <S> <stripes> <form> [...]

@@ -1,4 +1,4 @@
-"""Table of tools/pmc_forms.sh: per kernel form, % of 8 TB/s (trace), LDS-array busy, VALU
+"""Table of tools/jobs.sh pmc_forms: per kernel form, % of 8 TB/s (trace), LDS-array busy, VALU
 issue share, waves resident per SIMD, wait share and clock.
 usage: python tools/pmc_forms_table.py <gpurun_out/tag> <bytes per launch> <order> [...]
 LDS busy = SQ_LDS_IDX_ACTIVE / CU cycles; VALU share = SQ_ACTIVE_INST_VALU (quad-cycles x 4)

@@ -1,4 +1,4 @@
-"""Summarize a tools/profile.sh output dir into profiles/<round>/ (kernel stats + HBM
+"""Summarize a tools/jobs.sh profile output dir into profiles/<round>/ (kernel stats + HBM
 traffic from the separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected)."""
 import csv
 import json
@@ -50,7 +50,7 @@ def main(src, dst, k=10, m=4, S=1 << 20, B=256, erase=(0, 1, 2, 3), layout="plan
         "kernel_stats": {"calls": int(ks["Calls"]), "avg_ns": float(ks["AverageNs"]),
                          "min_ns": float(ks["MinNs"]), "max_ns": float(ks["MaxNs"])},
         "source": ("rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE and --pmc WRITE_SIZE in "
-                   "separate passes of bench.py (tools/profile.sh); the timed steps are the "
+                   "separate passes of bench.py (tools/jobs.sh profile); the timed steps are the "
                    "last 2 x steps plan launches of the trace, alternately encode and decode "
                    "(earlier dispatches: round-trip check, rs_plan_tune candidates, warmup); "
                    "kernel_stats covers every dispatch of the instance, tuning included"),
