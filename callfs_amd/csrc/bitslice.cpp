@@ -67,33 +67,51 @@ std::string cache_dir() {
   return std::string();
 }
 
-bool read_file(const std::string& path, std::vector<char>& out) {
+// A cache entry: a 16-B header ("CFBS", the waves-per-SIMD floor the search settled on, the
+// spilled VGPRs, the code object's size) and the code object. An entry that does not parse,
+// whose size disagrees or whose code is not an ELF object is a miss (then recompiled).
+constexpr char kCacheMagic[4] = {'C', 'F', 'B', 'S'};
+
+bool read_entry(const std::string& path, std::vector<char>& code, int* waves, int* spills) {
   std::ifstream f(path, std::ios::binary);
   if (!f) return false;
-  out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
-  return !out.empty();
+  std::vector<char> all((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  if (all.size() <= 16 || std::memcmp(all.data(), kCacheMagic, 4) != 0) return false;
+  int32_t hdr[3];
+  std::memcpy(hdr, all.data() + 4, sizeof hdr);
+  if (hdr[2] <= 0 || static_cast<size_t>(hdr[2]) != all.size() - 16) return false;
+  if (std::memcmp(all.data() + 16, "\x7f" "ELF", 4) != 0) return false;
+  code.assign(all.begin() + 16, all.end());
+  *waves = hdr[0];
+  *spills = hdr[1];
+  return true;
 }
 
-void write_file(const std::string& dir, const std::string& path, const std::vector<char>& data) {
+void write_entry(const std::string& dir, const std::string& path, const std::vector<char>& code,
+                 int waves, int spills) {
   if (dir.empty()) return;
-  // mkdir -p of the cache directory (two levels at most: <cache>/callfs_rs)
+  // mkdir -p of the cache directory
   std::string acc;
   std::stringstream ss(dir);
   std::string part;
-  if (!dir.empty() && dir[0] == '/') acc = "/";
+  if (dir[0] == '/') acc = "/";
   while (std::getline(ss, part, '/')) {
     if (part.empty()) continue;
     acc += part + "/";
     (void)::mkdir(acc.c_str(), 0755);
   }
   const std::string tmp = path + ".tmp." + std::to_string(::getpid());
+  const int32_t hdr[3] = {waves, spills, static_cast<int32_t>(code.size())};
+  bool ok;
   {
     std::ofstream f(tmp, std::ios::binary);
-    if (!f) return;
-    f.write(data.data(), static_cast<std::streamsize>(data.size()));
-    if (!f) return;
+    f.write(kCacheMagic, 4);
+    f.write(reinterpret_cast<const char*>(hdr), sizeof hdr);
+    f.write(code.data(), static_cast<std::streamsize>(code.size()));
+    f.close();
+    ok = static_cast<bool>(f);
   }
-  (void)std::rename(tmp.c_str(), path.c_str());
+  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) (void)std::remove(tmp.c_str());
 }
 
 }  // namespace
@@ -273,8 +291,12 @@ void Kernel::compile_locked(std::unique_lock<std::mutex>& lk) {
   std::vector<char> code;
   std::string err;
   int spills = -1;
-  if (path.empty() || !read_file(path, code)) {
+  int cached_waves = 0;
+  if (!path.empty() && read_entry(path, code, &cached_waves, &spills)) {
+    opt.min_waves = cached_waves;
+  } else {
     code.clear();
+    spills = -1;
     // lower the waves-per-SIMD floor while the compiler spills more than kSpillLimit VGPRs
     for (;;) {
       code = rtc_compile(src, opts, &err, &spills);
@@ -282,7 +304,7 @@ void Kernel::compile_locked(std::unique_lock<std::mutex>& lk) {
       --opt.min_waves;
       src = kernel_source(net, "rs_bs", opt, sizeof(Args));
     }
-    if (!code.empty() && !path.empty()) write_file(dir, path, code);
+    if (!code.empty() && !path.empty()) write_entry(dir, path, code, opt.min_waves, spills);
   }
   const double secs =
       std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -42,3 +42,39 @@ def test_bitslice_kernels_compile_for_gfx950(tmp_path):
     r = subprocess.run([str(exe), "10,9", "20,16", "33,12", "64,8"], capture_output=True,
                        text=True, env=env, timeout=600)
     assert r.returncode == 0 and "bs_compile ok" in r.stdout, r.stdout + r.stderr[-2000:]
+
+
+def test_bitslice_code_object_cache(tmp_path):
+    """The on-disk code-object cache (CALLFS_RS_JIT_CACHE): a second process loads the entry
+    the first wrote (same waves floor and spills, no compile), and a damaged entry is a miss
+    that is compiled and rewritten."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    exe = tmp_path / "bs_compile"
+    subprocess.run([hipcc, "-O1", "-std=c++17", "-x", "hip", "--offload-arch=gfx950", "-I", INC,
+                    os.path.join(ROOT, "tests", "native", "bs_compile.cpp"),
+                    os.path.join(INC, "bitslice.cpp"), "-lhiprtc", "-o", str(exe)],
+                   check=True, capture_output=True)
+    cache = tmp_path / "cache"
+    env = dict(os.environ, CALLFS_RS_JIT_CACHE=str(cache), CALLFS_OFFLOAD_ARCH="gfx950")
+
+    def run():
+        r = subprocess.run([str(exe), "20,16"], capture_output=True, text=True, env=env,
+                           timeout=600)
+        assert r.returncode == 0 and "bs_compile ok" in r.stdout, r.stdout + r.stderr[-2000:]
+        line = r.stdout.splitlines()[0]
+        fields = dict(f.split("=") for f in line.split() if "=" in f)
+        return fields["waves"], fields["spills"], float(line.split()[-2])
+
+    w1, s1, t1 = run()
+    entries = [p for p in cache.iterdir() if p.suffix == ".co"]
+    assert len(entries) == 1, entries
+    blob = entries[0].read_bytes()
+    assert blob[:4] == b"CFBS" and blob[16:20] == b"\x7fELF"
+    w2, s2, t2 = run()
+    assert (w2, s2) == (w1, s1) and t2 < t1 / 4, (t1, t2)
+    entries[0].write_bytes(blob[:len(blob) // 2])  # truncated: a miss, compiled again
+    w3, s3, t3 = run()
+    assert (w3, s3) == (w1, s1)
+    assert entries[0].read_bytes() == blob
