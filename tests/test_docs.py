@@ -111,3 +111,20 @@ def test_integration_tables_are_contiguous():
             # a table starts here: it needs a header separator on the next line
             assert i + 1 < len(lines) and re.match(r"^\|[\s:|-]+\|$", lines[i + 1]), \
                 f"INTEGRATION.md:{i + 1}: table rows without a header"
+
+
+def test_jobs_script_parses_and_lists_its_jobs():
+    """The jobs script (tools/jobs.sh) parses, and with no job named it lists every job it
+    defines."""
+    import shutil
+    import subprocess
+    if shutil.which("bash") is None:
+        import pytest
+        pytest.skip("bash not available")
+    path = os.path.join(ROOT, "tools", "jobs.sh")
+    subprocess.run(["bash", "-n", path], check=True)
+    r = subprocess.run(["bash", path], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2
+    listed = {ln.strip() for ln in r.stderr.splitlines()[1:]}
+    defined = set(re.findall(r"^job_([a-z0-9_]+)\(\) \{$", open(path).read(), flags=re.M))
+    assert listed == defined and len(defined) >= 30, (listed ^ defined)
