@@ -12,8 +12,9 @@
 //
 // Persistence: CALLFS_RS_TUNE_TABLE names a text file, one entry per line
 // ("device K R tps_log2 align kind mis order"), read on first use and rewritten whole (temp
-// file + rename) after each change, so a deployment tunes once per box and every later process
-// starts from the measured forms. Unset: the table lives for the process.
+// file + rename) after each change, merged with what other processes wrote to it meanwhile, so
+// a deployment tunes once per box and every later process starts from the measured forms.
+// Unset: the table lives for the process.
 #pragma once
 
 #include <cstdint>
@@ -83,6 +84,7 @@ class TuneTable {
     if (e.order == order && e.key.K == k.K) return;
     e.key = k;
     e.order = order;
+    e.ours = true;
     save_locked();
   }
   // Forgets every entry (and the file's path: tests point tables at their own files).
@@ -102,6 +104,7 @@ class TuneTable {
   struct Entry {
     TuneKey key;
     int order = -1;
+    bool ours = false;  // recorded by this process (else read from the file)
   };
   void load_locked() {
     if (loaded_) return;
@@ -110,6 +113,11 @@ class TuneTable {
       const char* e = std::getenv("CALLFS_RS_TUNE_TABLE");
       if (e) path_ = e;
     }
+    read_file(false);
+  }
+  // Adds the file's entries; `keep_ours`: an entry this process recorded wins over the file's
+  // (an entry it only read is replaced by the file's, which may be newer).
+  void read_file(bool keep_ours) {
     if (path_.empty()) return;
     FILE* f = std::fopen(path_.c_str(), "r");
     if (!f) return;
@@ -118,12 +126,16 @@ class TuneTable {
     while (std::fscanf(f, "%d %d %d %d %d %d %d %d", &k.device, &k.K, &k.R, &k.tps_log2, &k.align,
                        &k.kind, &k.mis, &order) == 8) {
       if (k.K < 1 || k.K > 256 || k.R < 1 || k.R > 16 || order < 0) continue;
+      auto it = map_.find(k.packed());
+      if (keep_ours && it != map_.end() && it->second.ours) continue;
       map_[k.packed()] = Entry{k, order};
     }
     std::fclose(f);
   }
   void save_locked() {
     if (path_.empty()) return;
+    // what other processes recorded since this one read the file is kept, not overwritten
+    read_file(true);
     // one temp file per process: processes sharing a table file never write the same temp
     const std::string tmp = path_ + "." + std::to_string(static_cast<long>(getpid())) + ".tmp";
     FILE* f = std::fopen(tmp.c_str(), "w");

@@ -636,6 +636,24 @@ int main() {
     TuneTable u;
     u.reset(path);
     CHECK(u.size() == 2 && u.lookup(a) == 258 && u.lookup(b) == 257);
+    // two processes' tables on one file: each rewrite keeps the entries the other recorded
+    const TuneKey c = tune_key(0, 6, 3, 64, 20, false, false, false, false);
+    const TuneKey d = tune_key(0, 8, 4, 64, 20, false, false, false, false);
+    u.record(c, 3);        // u read the file before t recorded d
+    t.record(d, 5);        // t's rewrite merges u's c
+    CHECK(t.lookup(c) == 3 && t.lookup(d) == 5);
+    u.record(a, 96);       // u's own newer choice for a wins over the file's 258
+    TuneTable v;
+    v.reset(path);
+    CHECK(v.size() == 4 && v.lookup(a) == 96 && v.lookup(b) == 257 && v.lookup(c) == 3 &&
+          v.lookup(d) == 5);
+    // an entry a table only read is not written back over a newer one: u read b = 257 and
+    // never recorded it; v re-tunes b, and u's next rewrite (for another key) keeps v's 99
+    v.record(b, 99);
+    u.record(tune_key(0, 5, 2, 64, 20, false, false, false, false), 1);
+    TuneTable w;
+    w.reset(path);
+    CHECK(w.lookup(b) == 99 && w.size() == 5);
     u.reset(nullptr);  // memory only (CALLFS_RS_TUNE_TABLE unset in this test)
     CHECK(u.empty());
     // concurrent tuners and launches
@@ -652,7 +670,6 @@ int main() {
     for (auto& x : ths) x.join();
     CHECK(t.size() > 2);
     std::remove(path);
-    std::remove((std::string(path) + ".tmp").c_str());
   }
 
   std::printf(fails ? "FAILED %d\n" : "host_test ok\n", fails);
