@@ -73,6 +73,34 @@ def test_wide_encode_and_decode_vs_oracle(native_lib, k, m):
             assert np.array_equal(sb.gather().cpu().numpy(), host), (name, list(lost))
 
 
+@pytest.mark.parametrize("k,m", [(1, 16), (2, 12), (3, 9), (4, 13), (6, 9)])
+def test_few_inputs_many_rows_vs_oracle(native_lib, k, m):
+    """Groups of 9..16 rows over 1..6 inputs (any m >= 1 per request,
+    post_file_enhanced.go:36-44): the rule's bit-sliced kernel for the encode and for a decode
+    that loses every data shard it can, and two pinned orders; k <= 3 is where the nibble path
+    would be the v_perm kernel (rs_apply_vec)."""
+    from callfs_amd.device import Plan
+    S = 2 * 8192 + 16 * 5 + 3
+    batch = 3
+    n = k + m
+    sb, host = _consistent(k, m, S, batch, seed=k * 17 + m)
+    enc = Plan.for_batch(sb)
+    assert enc.forms() == ["bs-g8"], enc.forms()
+    erase = list(range(k)) + list(range(k, k + m - k))  # all data, then parity up to m lost
+    assert len(erase) == m
+    dec = Plan.for_batch(sb, present=[i not in erase for i in range(n)])
+    assert all(f.startswith("bs") for f in dec.forms()), dec.forms()
+    for name in ("rule", "bs-x32", "bs"):
+        for p, lost in ((enc, range(k, n)), (dec, erase)):
+            if name != "rule":
+                _pin(p, name)
+            for i in lost:
+                sb.zero_shard(i)
+            p.launch()
+            assert not p.corrupt(), (name, lost)
+            assert np.array_equal(sb.gather().cpu().numpy(), host), (name, list(lost))
+
+
 @pytest.mark.parametrize("k,m,erase", [(20, 16, 12), (32, 12, 9), (10, 16, 14)])
 def test_wide_decode_verify_rows_flag_corruption(native_lib, k, m, erase):
     """Fewer erasures than m: the present parity beyond the first k are Verify rows compared
