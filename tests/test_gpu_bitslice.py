@@ -432,6 +432,19 @@ def test_host_memory_paths_with_bitslice_sync(native_lib, tmp_path):
         "dmg = [[None if i in (0, 5, 9, 20, 21, 22, 23, 24, 25, 26) else s for i, s in enumerate(f)] for f in full]\n"
         "assert E.reconstruct_batch(dmg, 20, 12) == [0] * 5\n"
         "assert all(bytes(dmg[b][i]) == full[b][i] for b in range(5) for i in range(32))\n"
+        "# the download path of every profile: Decode with nothing lost is a read-only Verify\n"
+        "# launch (the bit-sliced kernel at every R); a flipped parity byte must be reported\n"
+        "from callfs_amd import ErrShardCorrupted\n"
+        "for k, m, L in ((1, 1, 5000), (2, 1, 70_001), (4, 2, 1 << 20), (10, 4, 3 * (1 << 20) + 1), (16, 4, 999_999), (10, 8, 2 * (1 << 20))):\n"
+        "    data = rng.integers(0, 256, L, dtype=np.uint8).tobytes()\n"
+        "    sh = [bytearray(s) for s in c.encode(data, ErasureProfile(k, m))]\n"
+        "    assert c.decode(list(sh), ErasureProfile(k, m), L) == data, (k, m)\n"
+        "    sh[k + m - 1][len(sh[0]) // 2] ^= 0x40\n"
+        "    try:\n"
+        "        c.decode(list(sh), ErasureProfile(k, m), L)\n"
+        "        raise SystemExit(f'corruption not flagged {k},{m}')\n"
+        "    except ErrShardCorrupted:\n"
+        "        pass\n"
         "print('sync ok')\n")
     env = dict(os.environ, CALLFS_RS_BITSLICE="sync", CALLFS_RS_JIT_CACHE="0")
     r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, env=env,
