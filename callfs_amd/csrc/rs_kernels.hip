@@ -660,6 +660,7 @@ int bitslice_order(TileOrder o) {
     case TileOrder::kGroup8: return 5;
     case TileOrder::kSeg16: return 6;
   }
+  return -1;  // not a TileOrder (a code outside 256 + [0, kTileOrders))
 }
 }  // namespace
 
@@ -897,6 +898,7 @@ hipError_t launch_apply(ApplyArgs a, hipStream_t stream, bool bytes_only, int or
   // choice runs it once compiled and the nibble-table kernel until then
   if (!bytes_only && (order >= kOrderBitslice || (order < 0 && takes_bitslice(a)))) {
     const bool pinned = order >= kOrderBitslice;
+    if (pinned && order >= kOrderBitslice + kTileOrders) return hipErrorInvalidValue;
     const TileOrder bo = pinned ? static_cast<TileOrder>(order - kOrderBitslice) : bitslice_rule_order(a);
     hipError_t e = hipSuccess;
     if (launch_bitslice(a, stream, bo, ev, pinned || bs::mode() == bs::Mode::kSync, &e)) return e;
