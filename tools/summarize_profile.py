@@ -110,11 +110,13 @@ def main(src, dst, k=10, m=4, S=1 << 20, B=256, erase=(0, 1, 2, 3), layout="plan
 
 
 if __name__ == "__main__":
-    # usage: summarize_profile.py <profile dir> <dst dir> [k m shard_bytes stripes erase]
+    # usage: summarize_profile.py <profile dir> <dst dir> [k m shard_bytes stripes erase layout kernel]
     a = sys.argv[1:]
     extra = [int(x) for x in a[2:6]]
     if len(a) > 6:
         extra.append(tuple(int(x) for x in a[6].split(",")))
     if len(a) > 7:
         extra.append(a[7])
+    if len(a) > 8:  # the kernel name filter: "rs_bs" for the bit-sliced kernels
+        extra.append(a[8])
     main(a[0], a[1], *extra)
