@@ -116,22 +116,33 @@ void write_entry(const std::string& dir, const std::string& path, const std::vec
 
 }  // namespace
 
-// One background thread compiles queued kernels in order. It is joined at exit after the
-// compile in flight (queued ones are dropped), so no hiprtc call outlives the process's
-// static teardown.
+// One background thread compiles queued kernels in order.
+//
+// Exit: the process's static destructors include hiprtc / comgr's, some of them registered
+// during the first compile. A compile still running on the worker while they run used freed
+// comgr memory (SIGSEGV or a double free at exit, tests/native/bs_worker.cpp), so the worker
+// is never destroyed; instead the first push compiles a small kernel (comgr's lazy state now
+// exists) and then registers drain() with atexit. Handlers run in reverse order of
+// registration, so drain() -- drop the queue, let the compile in flight finish, join --
+// runs before comgr's destructors.
 class Worker {
  public:
   static Worker& get() {
-    static Worker w;
-    return w;
+    static Worker* w = new Worker;  // never destroyed (see above)
+    return *w;
   }
   void push(const std::shared_ptr<Kernel>& k) {
+    std::call_once(init_, [] {
+      warm_compiler();
+      std::atexit([] { Worker::get().drain(); });
+    });
     std::lock_guard<std::mutex> g(mu_);
+    if (stop_) return;  // exiting: the kernel stays queued, launches keep the nibble tables
     if (!th_.joinable()) th_ = std::thread([this] { loop(); });
     q_.push_back(k);
     cv_.notify_one();
   }
-  ~Worker() {
+  void drain() {
     {
       std::lock_guard<std::mutex> g(mu_);
       stop_ = true;
@@ -142,6 +153,7 @@ class Worker {
   }
 
  private:
+  static void warm_compiler();
   void loop() {
     for (;;) {
       std::shared_ptr<Kernel> k;
@@ -155,6 +167,7 @@ class Worker {
       if (k) k->compile_now();
     }
   }
+  std::once_flag init_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::weak_ptr<Kernel>> q_;
@@ -264,6 +277,21 @@ int auto_waves(int R, int prefetch) {
 }
 constexpr int kSpillLimit = 16;  // VGPRs spilled that a floor may cost before it is lowered
 }  // namespace
+
+void Worker::warm_compiler() {
+  // the constructs the generated kernels use (a bit-select, non-temporal 16-B loads and stores)
+  static const char* src =
+      "typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));\n"
+      "extern \"C\" __global__ void warm(const u32x4* a, u32x4* b) {\n"
+      "  u32x4 x = __builtin_nontemporal_load(a + threadIdx.x);\n"
+      "  x.x = __builtin_amdgcn_bitop3_b32(x.x, x.y, x.z, 0xCA);\n"
+      "  __builtin_nontemporal_store(x, b + threadIdx.x);\n"
+      "}\n";
+  std::string err;
+  int spills = 0;
+  (void)rtc_compile(src, {"--offload-arch=" + target_arch(), "-O3", "-std=c++17", "-fno-gpu-rdc"},
+                    &err, &spills);
+}
 
 void Kernel::compile_locked(std::unique_lock<std::mutex>& lk) {
   state_ = State::kCompiling;

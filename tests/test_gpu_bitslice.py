@@ -500,3 +500,30 @@ def test_read_only_verify_rule_and_flags(native_lib, k, m, S, layout):
         sb.shard(b, i)[pos] ^= 0x10
     ver.launch()
     assert not ver.corrupt()
+
+
+def test_process_exits_cleanly_during_background_compiles(native_lib, tmp_path):
+    """A short-lived process (one host-memory call, then exit) leaves bit-sliced compiles
+    queued or running on the worker: it must exit 0 with no crash in comgr's teardown
+    (bitslice.cpp Worker: drained by an atexit handler registered after comgr initialised)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prog = tmp_path / "short.py"
+    prog.write_text(
+        "import sys, numpy as np\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "import torch\n"
+        "from callfs_amd import Codec, ErasureProfile\n"
+        "rng = np.random.default_rng(5)\n"
+        "c = Codec()\n"
+        "for k, m in ((20, 16), (10, 4), (32, 9)):\n"
+        "    data = rng.integers(0, 256, 3 << 20, dtype=np.uint8).tobytes()\n"
+        "    sh = c.encode(data, ErasureProfile(k, m))\n"
+        "    assert c.decode(list(sh), ErasureProfile(k, m), len(data)) == data\n"
+        "print('short ok', flush=True)\n")
+    env = dict(os.environ, CALLFS_RS_JIT_CACHE="0")
+    for _ in range(2):
+        r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, env=env,
+                           timeout=300)
+        assert r.returncode == 0 and "short ok" in r.stdout, (r.returncode, r.stderr[-3000:])

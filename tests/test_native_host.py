@@ -78,3 +78,24 @@ def test_bitslice_code_object_cache(tmp_path):
     w3, s3, t3 = run()
     assert (w3, s3) == (w1, s1)
     assert entries[0].read_bytes() == blob
+
+
+def test_bitslice_compile_worker_under_tsan(tmp_path):
+    """The bit-sliced kernels' compile state machine (bitslice.cpp Kernel / Worker /
+    kernel_for) from eight threads under ThreadSanitizer, hiprtc compiling on the CPU: every
+    kernel ends Ready once, one Kernel per coefficient block, and a background compile still
+    queued or running at exit neither crashes nor races comgr's teardown (round 6 found the
+    worker compiling while comgr's static destructors ran: SIGSEGV or a double free at exit)."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    exe = tmp_path / "bs_worker"
+    subprocess.run([hipcc, "-O1", "-g", "-std=c++17", "-x", "hip", "--offload-arch=gfx950",
+                    "-Xarch_host", "-fsanitize=thread", "-I", INC,
+                    os.path.join(ROOT, "tests", "native", "bs_worker.cpp"),
+                    os.path.join(INC, "bitslice.cpp"), "-lhiprtc", "-o", str(exe)],
+                   check=True, capture_output=True)
+    env = dict(os.environ, CALLFS_RS_JIT_CACHE="0", CALLFS_OFFLOAD_ARCH="gfx950")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=900)
+    assert r.returncode == 0 and "bs_worker ok" in r.stdout, r.stdout + r.stderr[-3000:]
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
