@@ -137,8 +137,13 @@ class Worker {
       std::atexit([] { Worker::get().drain(); });
     });
     std::lock_guard<std::mutex> g(mu_);
-    if (stop_) return;  // exiting: the kernel stays queued, launches keep the nibble tables
-    if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+    // exiting, or a fork's child (the thread is the parent's): the kernel stays queued and
+    // launches keep the nibble tables
+    if (stop_ || (th_.joinable() && owner_ != ::getpid())) return;
+    if (!th_.joinable()) {
+      th_ = std::thread([this] { loop(); });
+      owner_ = ::getpid();
+    }
     q_.push_back(k);
     cv_.notify_one();
   }
@@ -149,7 +154,8 @@ class Worker {
       q_.clear();
     }
     cv_.notify_all();
-    if (th_.joinable()) th_.join();
+    // a fork's child exits without the parent's thread (never joined: the Worker is immortal)
+    if (th_.joinable() && owner_ == ::getpid()) th_.join();
   }
 
  private:
@@ -172,6 +178,7 @@ class Worker {
   std::condition_variable cv_;
   std::deque<std::weak_ptr<Kernel>> q_;
   std::thread th_;
+  pid_t owner_ = 0;  // the process that started th_
   bool stop_ = false;
 };
 

@@ -5,11 +5,16 @@
 // Eight threads ask for kernels of four coefficient blocks (two of them the same block under
 // different vectors, which must map to one Kernel), queue background compiles, wait on
 // synchronous ones and poll states in every interleaving; every kernel must end Ready exactly
-// once with a code object, and the process must exit with the worker joined.
+// once with a code object, a forked child must exit cleanly, and the process must exit with
+// the worker joined.
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <thread>
 #include <vector>
+
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include "bitslice.hpp"
 
@@ -52,6 +57,19 @@ int main() {
       if (s == 0 && seen[t * 4 + rep] != k0) bad++;
     }
   if (!k0 || k0 != k2) bad++;
+  // a fork's child (the worker thread is the parent's): a compile request is ignored and
+  // exit's drain does not join a thread the child does not have
+  const pid_t pid = fork();
+  if (pid == 0) {
+    std::vector<uint8_t> c(11 * 9, 3);
+    bs::kernel_for(11, 9, c.data())->compile_async();
+    std::exit(0);
+  }
+  int status = -1;
+  if (pid < 0 || waitpid(pid, &status, 0) != pid || !WIFEXITED(status) || WEXITSTATUS(status) != 0) {
+    std::printf("forked child: status %d\n", status);
+    bad++;
+  }
   // a queued compile of a fresh block still in the worker's queue at exit is dropped, the
   // compile in flight finishes and the worker is joined (static teardown)
   std::vector<uint8_t> late(14 * 9, 7);
