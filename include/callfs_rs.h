@@ -196,7 +196,9 @@ void rs_plan_destroy(rs_plan* plan);
 #define RS_ORDER_REALIGN 32
 /* the launch group's bit-sliced kernel: an XOR network over bit planes
  * generated for the group's coefficient block and compiled at plan time (hiprtc; cached on
- * disk), RS_ORDER_BITSLICE + the tile order it runs in (RS_ORDER_0..6) */
+ * disk; blocks of more than 2,048 coefficients compile in the background while the plan runs
+ * the nibble-table kernels), RS_ORDER_BITSLICE + the tile order it runs in (RS_ORDER_0..6);
+ * pinning one waits for its compile */
 #define RS_ORDER_BITSLICE 256
 int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups);
 /* Sets the tile order of launch groups 0..n-1 (the others: the rule) to orders[i], as

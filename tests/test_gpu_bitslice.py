@@ -527,3 +527,22 @@ def test_process_exits_cleanly_during_background_compiles(native_lib, tmp_path):
         r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, env=env,
                            timeout=300)
         assert r.returncode == 0 and "short ok" in r.stdout, (r.returncode, r.stderr[-3000:])
+
+
+def test_large_block_compiles_in_background(native_lib):
+    """A coefficient block of more than 2,048 entries (RS(180,16): 2,880) is compiled in the
+    background at rs_plan_create: the plan runs whichever kernel is ready and every launch is
+    bit-exact; pinning the bit-sliced order waits for the compile."""
+    from callfs_amd.device import Plan
+    k, m, S, batch = 180, 16, 16_384 + 48, 2
+    sb, host = _consistent(k, m, S, batch, seed=180)
+    enc = Plan.for_batch(sb)
+    assert enc.forms()[0] in ("bs-g8", "consecutive", "g8", "g2", "x32", "q8"), enc.forms()
+    for name in ("rule", "bs-g8"):
+        if name != "rule":
+            _pin(enc, name)
+        for i in range(k, k + m):
+            sb.zero_shard(i)
+        enc.launch()
+        assert np.array_equal(sb.gather().cpu().numpy(), host), name
+    assert enc.forms() == ["bs-g8"], enc.forms()
