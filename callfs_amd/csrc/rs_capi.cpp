@@ -1754,7 +1754,14 @@ int rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_gro
   int rc = RS_OK;
   for (size_t gi = 0; gi < t.groups.size() && rc == RS_OK; ++gi) {
     const ApplyArgs a = group_args(t, plan->layout, gi, plan->batch, d, plan->S, 1, plan->hint);
-    const std::vector<int> cand = order_candidates(a);
+    std::vector<int> cand = order_candidates(a);
+    // the bit-sliced orders only when the group's kernel compiles and loads here: a hiprtc
+    // that fails on some box leaves the tuner (and the bench) on the nibble-table forms
+    const Group& grp = t.groups[gi];
+    const auto bs_order = [](int o) { return o >= kOrderBitslice; };
+    if (std::any_of(cand.begin(), cand.end(), bs_order) &&
+        (!grp.bsk || !grp.bsk->function(plan->device, /*wait=*/true)))
+      cand.erase(std::remove_if(cand.begin(), cand.end(), bs_order), cand.end());
     if (cand.size() < 2) continue;
     std::vector<float> best(cand.size(), 1e30f);
     // warm-up in the rule's order first, by time: a chip that has just come out of other

@@ -546,3 +546,44 @@ def test_large_block_compiles_in_background(native_lib):
         enc.launch()
         assert np.array_equal(sb.gather().cpu().numpy(), host), name
     assert enc.forms() == ["bs-g8"], enc.forms()
+
+
+def test_compile_failure_falls_back_to_nibble_tables(native_lib, tmp_path):
+    """A box where hiprtc cannot build the bit-sliced kernels (here: gfx942 forced through
+    CALLFS_OFFLOAD_ARCH, a target without v_bitop3, so every compile fails) keeps every path
+    on the nibble-table kernels: the
+    plan's rule, rs_plan_tune (which drops the bit-sliced candidates instead of failing, so
+    bench.py still runs) and the host-memory calls, all bit-exact."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prog = tmp_path / "nocompile.py"
+    prog.write_text(
+        "import sys, numpy as np\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "import torch\n"
+        "from oracle import cref\n"
+        "from callfs_amd import Codec, ErasureProfile\n"
+        "from callfs_amd.device import Plan, StripeBatch\n"
+        "k, m, S = 20, 16, 65_536 + 5\n"
+        "sb = StripeBatch(k, m, S, 2, torch.device('cuda:0'))\n"
+        "sb.fill_random(9)\n"
+        "p = Plan.for_batch(sb)\n"
+        "assert not p.forms()[0].startswith('bs'), p.forms()\n"
+        "orders = p.tune()\n"
+        "assert not any(o.startswith('bs') for o in orders), orders\n"
+        "p.launch(); torch.cuda.synchronize()\n"
+        "h = sb.buf[1, :, :S].cpu().numpy()\n"
+        "want = cref.encode([h[i] for i in range(k)], k, m)\n"
+        "assert all(np.array_equal(h[k + j], want[j]) for j in range(m))\n"
+        "rng = np.random.default_rng(3)\n"
+        "data = rng.integers(0, 256, 2 << 20, dtype=np.uint8).tobytes()\n"
+        "c = Codec()\n"
+        "sh = c.encode(data, ErasureProfile(k, m))\n"
+        "lost = list(sh); lost[0] = lost[3] = lost[k] = None\n"
+        "assert c.decode(lost, ErasureProfile(k, m), len(data)) == data\n"
+        "print('nocompile ok', flush=True)\n")
+    env = dict(os.environ, CALLFS_RS_JIT_CACHE="0", CALLFS_OFFLOAD_ARCH="gfx942")
+    r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 0 and "nocompile ok" in r.stdout, r.stdout + r.stderr[-3000:]
