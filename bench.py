@@ -464,9 +464,16 @@ def main(argv=None):
         del ref
 
     # untimed: pick each plan's tile order on this box (the outputs are recomputed to the
-    # same bytes; DESIGN.md §6.2 "Tile order")
-    orders = ({"encode": enc.tune(stream=stream), "decode": dec.tune(stream=stream)}
-              if args.tune else None)
+    # same bytes; DESIGN.md §6.2 "Tile order"). Tuning is optional: if it fails the plans
+    # keep the rule's forms and the line says why (config.tune_error)
+    tune_error = None
+    try:
+        orders = ({"encode": enc.tune(stream=stream), "decode": dec.tune(stream=stream)}
+                  if args.tune else None)
+    except N.NativeError as e:
+        orders, tune_error = None, str(e)[:200]
+        enc.set_orders(["none"] * len(enc.forms()))
+        dec.set_orders(["none"] * len(dec.forms()))
 
     for _ in range(args.warmup):
         enc.launch(stream)
@@ -553,6 +560,7 @@ def main(argv=None):
             "decode_verify_rows": verify_rows,
             # per launch group, chosen by rs_plan_tune before the warmup (None: the rule)
             "tile_order": orders,
+            **({"tune_error": tune_error} if tune_error else {}),
             # the kernel form each launch group ran in the timed steps (rs_plan_forms: a tile
             # order of the nibble-table kernels, or "bs-*" for the bit-sliced ones)
             "forms": {"encode": enc.forms(), "decode": dec.forms()},
