@@ -1,7 +1,8 @@
 // Bit-sliced GF(2^8) kernels compiled at plan time: the runtime around
 // bitslice_gen.hpp. One Kernel per distinct coefficient block (K inputs x R rows), compiled
-// once per process by hiprtc for gfx950 (and kept in an on-disk cache of code objects),
-// loaded into each device on first use.
+// once per process by hiprtc for the device's gfx target (and kept in an on-disk cache of code
+// objects), loaded into each device on first use. tests/native/bs_worker.cpp drives the
+// compile state machine from eight threads under ThreadSanitizer.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -32,7 +33,9 @@ class Kernel : public std::enable_shared_from_this<Kernel> {
   int block_threads() const { return opt_.block; }
   int tile_vecs() const { return opt_.tile_vecs(); }
   State state() const;
-  // Queues the compile on the background worker (no-op once queued or done).
+  // Queues the compile on the background worker (no-op once queued or done). The worker is
+  // drained at exit before hiprtc's own teardown; requests made while exiting, or in a fork's
+  // child, are dropped (the kernel then stays on the nibble-table forms).
   void compile_async();
   // Compiles on the calling thread if nobody has (waits for a compile in flight); true when
   // the code object exists.
