@@ -6,6 +6,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -40,7 +41,14 @@ uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
 // the worker makes no HIP call, so one still compiling at process exit cannot race the HIP
 // runtime's teardown.
 std::string device_arch() {
-  if (const char* e = std::getenv("CALLFS_OFFLOAD_ARCH")) return e;
+  // only a well-formed target name (gfx + 3 or 4 hex digits: gfx90a, gfx950, gfx1201): hiprtc
+  // on a GPU box crashed on "gfx1" instead of failing the compile
+  if (const char* e = std::getenv("CALLFS_OFFLOAD_ARCH")) {
+    const std::string a = e;
+    bool ok = (a.size() == 6 || a.size() == 7) && a.compare(0, 3, "gfx") == 0;
+    for (size_t i = 3; ok && i < a.size(); ++i) ok = std::isxdigit(static_cast<unsigned char>(a[i])) != 0;
+    if (ok) return a;
+  }
   int dev = -1;
   hipDeviceProp_t p;
   if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) {
