@@ -587,3 +587,50 @@ def test_compile_failure_falls_back_to_nibble_tables(native_lib, tmp_path):
     r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, env=env,
                        timeout=300)
     assert r.returncode == 0 and "nocompile ok" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
+def test_concurrent_decodes_with_background_compiles(native_lib):
+    """A repair server's traffic: eight request threads decoding wide objects with a different
+    erasure set each call (a new coefficient block, so a background compile, then a module
+    load once it is ready) while the others launch; every object comes back bit-exact."""
+    import threading
+    from callfs_amd import Codec, ErasureProfile
+    k, m = 20, 12
+    prof = ErasureProfile(k, m)
+    rng = np.random.default_rng(77)
+    objs = [rng.integers(0, 256, (1 << 20) + 37 * i, dtype=np.uint8).tobytes() for i in range(4)]
+    c = Codec()
+    shards = [c.encode(o, prof) for o in objs]
+    errors = []
+
+    # ten erasure sets shared by the threads: the first calls of each run the nibble tables
+    # while its kernel compiles, later ones the bit-sliced kernel (loaded by whichever thread
+    # launches first); 5 s of traffic covers both
+    pr = np.random.default_rng(99)
+    pool = [pr.choice(k + m, size=int(pr.integers(1, m + 1)), replace=False) for _ in range(10)]
+    import time
+    t_end = time.time() + 5.0
+    calls = [0] * 8
+
+    def worker(t):
+        r = np.random.default_rng(1000 + t)
+        try:
+            it = 0
+            while time.time() < t_end:
+                i = (t + it) % len(objs)
+                lost = pool[int(r.integers(0, len(pool)))]
+                sh = [None if j in lost else s for j, s in enumerate(shards[i])]
+                if c.decode(sh, prof, len(objs[i])) != objs[i]:
+                    errors.append((t, it, sorted(lost.tolist())))
+                it += 1
+            calls[t] = it
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append((t, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    assert min(calls) > 10, calls
