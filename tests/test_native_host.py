@@ -46,8 +46,8 @@ def test_bitslice_kernels_compile_for_gfx950(tmp_path):
 
 def test_bitslice_code_object_cache(tmp_path):
     """The on-disk code-object cache (CALLFS_RS_JIT_CACHE): a second process loads the entry
-    the first wrote (same waves floor and spills, no compile), and a damaged entry is a miss
-    that is compiled and rewritten."""
+    the first wrote (same waves floor and spills; an edited header field shows the entry, not
+    a compile, was used), and a damaged entry is a miss that is compiled and rewritten."""
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("hipcc not available")
@@ -67,15 +67,22 @@ def test_bitslice_code_object_cache(tmp_path):
         fields = dict(f.split("=") for f in line.split() if "=" in f)
         return fields["waves"], fields["spills"], float(line.split()[-2])
 
-    w1, s1, t1 = run()
+    w1, s1, _ = run()
     entries = [p for p in cache.iterdir() if p.suffix == ".co"]
     assert len(entries) == 1, entries
     blob = entries[0].read_bytes()
     assert blob[:4] == b"CFBS" and blob[16:20] == b"\x7fELF"
-    w2, s2, t2 = run()
-    assert (w2, s2) == (w1, s1) and t2 < t1 / 4, (t1, t2)
+    w2, s2, _ = run()
+    assert (w2, s2) == (w1, s1), (w1, s1, w2, s2)
+    # the second process read the entry, not the compiler: a waves field edited in the file's
+    # header is what it reports
+    import struct
+    edited = blob[:4] + struct.pack("<i", 7) + blob[8:]
+    entries[0].write_bytes(edited)
+    w2b, _, _ = run()
+    assert w2b == "7", w2b
     entries[0].write_bytes(blob[:len(blob) // 2])  # truncated: a miss, compiled again
-    w3, s3, t3 = run()
+    w3, s3, _ = run()
     assert (w3, s3) == (w1, s1)
     assert entries[0].read_bytes() == blob
 
