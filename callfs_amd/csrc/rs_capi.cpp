@@ -1617,15 +1617,21 @@ int rs_plan_create(rs_ctx* ctx, int device, int k, int m, size_t S, int batch,
   }
   // plans are launched many times: the launch groups the rule gives the bit-sliced kernel have
   // it compiled (or loaded from the code cache) here, so every launch runs it; a compile that
-  // fails leaves them on the nibble-table kernels. Blocks of more than kSyncCompileMaxKR
-  // coefficients compile in the background instead (RS(200,16): 8 s on the GPU box, RS(240,16)
-  // 48 s on a build host): the plan runs the nibble-table kernels until the code is ready.
-  constexpr int kSyncCompileMaxKR = 2048;
+  // fails leaves them on the nibble-table kernels. A plan waits for at most kSyncCompileKR
+  // coefficients' worth of compiles (about 4 s on the GPU box); its other blocks compile in
+  // the background (RS(200,16) alone: 8 s there, RS(240,16) 48 s on a build host; the 8 groups
+  // of an RS(128,128) decode: 30 s) and run the nibble-table kernels until they are ready.
+  constexpr int kSyncCompileKR = 2048;
+  int sync_kr = 0;
   for (size_t gi = 0; gi < t->groups.size(); ++gi) {
     const Group& g = t->groups[gi];
-    if (g.bsk && bitslice_wanted(group_args(*t, plan->layout, gi, batch,
-                                            static_cast<uint8_t*>(plan->dmeta), S, 1, plan->hint)))
-      (void)g.bsk->function(device, /*wait=*/k * static_cast<int>(g.shard.size()) <= kSyncCompileMaxKR);
+    if (!g.bsk || !bitslice_wanted(group_args(*t, plan->layout, gi, batch,
+                                              static_cast<uint8_t*>(plan->dmeta), S, 1, plan->hint)))
+      continue;
+    const int kr = k * static_cast<int>(g.shard.size());
+    const bool wait = sync_kr + kr <= kSyncCompileKR;
+    if (wait) sync_kr += kr;
+    (void)g.bsk->function(device, wait);
   }
   *out = plan.release();
   return RS_OK;

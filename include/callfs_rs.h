@@ -196,8 +196,8 @@ void rs_plan_destroy(rs_plan* plan);
 #define RS_ORDER_REALIGN 32
 /* the launch group's bit-sliced kernel: an XOR network over bit planes
  * generated for the group's coefficient block and compiled at plan time (hiprtc; cached on
- * disk; blocks of more than 2,048 coefficients compile in the background while the plan runs
- * the nibble-table kernels), RS_ORDER_BITSLICE + the tile order it runs in (RS_ORDER_0..6);
+ * disk; past 2,048 coefficients per plan the blocks compile in the background while the plan
+ * runs the nibble-table kernels), RS_ORDER_BITSLICE + the tile order it runs in (RS_ORDER_0..6);
  * pinning one waits for its compile */
 #define RS_ORDER_BITSLICE 256
 int  rs_plan_tune(rs_plan* plan, void* stream, int reps, int* orders, int max_groups);

@@ -530,9 +530,9 @@ def test_process_exits_cleanly_during_background_compiles(native_lib, tmp_path):
 
 
 def test_large_block_compiles_in_background(native_lib):
-    """A coefficient block of more than 2,048 entries (RS(180,16): 2,880) is compiled in the
-    background at rs_plan_create: the plan runs whichever kernel is ready and every launch is
-    bit-exact; pinning the bit-sliced order waits for the compile."""
+    """A plan waits for at most 2,048 coefficients' worth of compiles; a larger block
+    (RS(180,16): 2,880) compiles in the background: the plan runs whichever kernel is ready
+    and every launch is bit-exact; pinning the bit-sliced order waits for the compile."""
     from callfs_amd.device import Plan
     k, m, S, batch = 180, 16, 16_384 + 48, 2
     sb, host = _consistent(k, m, S, batch, seed=180)
@@ -634,3 +634,27 @@ def test_concurrent_decodes_with_background_compiles(native_lib):
         th.join()
     assert not errors, errors
     assert min(calls) > 10, calls
+
+
+@pytest.mark.parametrize("k,m", [(255, 1), (128, 128)])
+def test_largest_profiles_pinned(native_lib, k, m):
+    """k + m = 256, the largest GF(2^8) profiles: one row over 255 inputs (encode and a
+    one-shard decode), and a decode that loses 128 of RS(128,128)'s shards, data and parity (8
+    launch groups of 16 rows over 128 inputs); every group pinned to its bit-sliced kernel,
+    against the oracle. (Sixteen 2,048-coefficient compiles would take a minute: the
+    RS(128,128) encode is left to the rule's paths.)"""
+    from callfs_amd.device import Plan
+    S, batch = 4096 + 16 * 3 + 5, 2
+    n = k + m
+    sb, host = _consistent(k, m, S, batch, seed=k)
+    lost = list(range(0, n, 2))[:m]
+    todo = [(None, lost)] if k == 128 else [("enc", range(k, n)), (None, lost)]
+    for what, gone in todo:  # plans made here: creating one compiles its rule's kernels
+        p = (Plan.for_batch(sb) if what == "enc"
+             else Plan.for_batch(sb, present=[i not in lost for i in range(n)]))
+        _pin(p, "bs-g2")
+        for i in gone:
+            sb.zero_shard(i)
+        p.launch()
+        assert not p.corrupt(), list(gone)[:4]
+        assert np.array_equal(sb.gather().cpu().numpy(), host), list(gone)[:4]
